@@ -1,0 +1,193 @@
+"""CPU fp32 restatement of the attack step loops and the adversarial fine-tune step.
+
+TEST INFRASTRUCTURE (see oracle/__init__.py).
+
+  * ``attack``      attack_rd.attack_ (attack_rd.py:381-575) + attack_our (:332-379)
+                    + self_ensemble.eval (self_ensemble.py:173-252).
+                    ``coupled=False`` (default): each image of the batch is an
+                    independent reference run (per-image loss_i, branch, loss);
+                    ``coupled=True``: the batch-mean semantics train.py:342 uses.
+  * ``ifgsm``       attack_ifgsm.attack_ifgsm / mifgsm_attack (attack_ifgsm.py:348-438).
+  * ``rd_loss``     train.RateDistortionLoss (train.py:37-96).
+  * ``adv_train_step``  train.py:335-366 (the working --adv path).
+"""
+from __future__ import annotations
+
+import math
+from types import SimpleNamespace
+
+import torch
+
+from . import codec
+from .msssim import ms_ssim, ms_ssim_per_image
+
+
+def lr_schedule(steps: int, lr: float):
+    """MultiStepLR([1,2,3], gamma=0.33) stepped when i % (steps//3) == 0 (attack_rd.py:503,553)."""
+    import warnings
+    p = torch.zeros(1, requires_grad=True)
+    opt = torch.optim.Adam([p], lr=lr)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1, 2, 3], gamma=0.33)
+    out = []
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(steps):
+            out.append(opt.param_groups[0]["lr"])
+            if i % max(steps // 3, 1) == 0:
+                sch.step()
+    return out
+
+
+def _per_image_mean(x):
+    return x.flatten(1).mean(1)
+
+
+def eval_batch(P, im_adv, im_s, output_s, model="hyper", clamp=True, adv=False, msssim=True):
+    """self_ensemble.eval (self_ensemble.py:173-252), evaluated per image."""
+    with torch.no_grad():
+        im_ = torch.clamp(im_adv, 0.0, 1.0) if clamp else im_adv
+        res = codec.forward(P, im_, model)
+        out = torch.clamp(res["x_hat"], 0.0, 1.0) if clamp else res["x_hat"]
+        H, W = im_adv.shape[2:]
+        B = im_adv.shape[0]
+        bpp = torch.stack([codec.bpp({k: v[b:b + 1] for k, v in res["likelihoods"].items()}, H * W)
+                           for b in range(B)])
+        mse_in = _per_image_mean((im_ - im_s) ** 2)
+        mse_out = _per_image_mean((out - output_s) ** 2)
+        if msssim:
+            msim_in = ms_ssim_per_image(im_, im_s)
+            msim_out = ms_ssim_per_image(out, output_s)
+        else:
+            msim_in = msim_out = torch.full((B,), float("nan"))
+        vi, vi_msim = [], []
+        for b in range(B):
+            mi, mo = float(mse_in[b]), float(mse_out[b])
+            v = vm = None
+            if mi > 1e-20 and mo > 1e-20:
+                v = 10.0 * math.log10(mo / mi)
+                if not adv and msssim and float(msim_in[b]) < 0.9999:
+                    vm = 10.0 * math.log10((1 - float(msim_out[b])) / (1 - float(msim_in[b])))
+            vi.append(v)
+            vi_msim.append(vm)
+    return SimpleNamespace(im=im_, out=out, bpp=bpp, mse_in=mse_in, mse_out=mse_out,
+                           msim_in=msim_in, msim_out=msim_out, vi=vi, vi_msim=vi_msim)
+
+
+def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
+           clamp=True, model="hyper", coupled=False, init_noise=None, eval_msssim=True,
+           record=None):
+    """attack_rd.attack_ restated (Adam on additive noise, L-inf box in the forward).
+
+    record: optional list; per step appends dict(loss_i, branch) for trajectory tests.
+    """
+    B = im_s.shape[0]
+    with torch.no_grad():
+        res = codec.forward(P, im_s, model)
+        output_s = torch.clamp(res["x_hat"], 0.0, 1.0) if clamp else res["x_hat"]
+        H, W = im_s.shape[2:]
+        bpp_ori = torch.stack([codec.bpp({k: v[b:b + 1] for k, v in res["likelihoods"].items()}, H * W)
+                               for b in range(B)])
+    noise_range = epsilon / 255.0
+    noise = torch.zeros_like(im_s) if init_noise is None else init_noise.clone()
+    noise.requires_grad_(True)
+    opt = torch.optim.Adam([noise], lr=lr)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1, 2, 3], gamma=0.33)
+    im_in = None
+    for i in range(steps):
+        noise_c = codec.UpBound.apply(codec.LowBound.apply(noise, -noise_range), noise_range)
+        im_in = codec.UpBound.apply(codec.LowBound.apply(im_s + noise_c, 0.0), 1.0)
+        if coupled:
+            loss_i = torch.mean((im_s - im_in) ** 2)
+            cheap = torch.full((B,), bool(loss_i > noise_thr))
+            li_b = loss_i.expand(B)
+        else:
+            li_b = _per_image_mean((im_s - im_in) ** 2)
+            cheap = li_b > noise_thr
+        losses = torch.zeros((), dtype=im_s.dtype)
+        if bool(cheap.any()):
+            idx = cheap.nonzero().flatten()
+            if att_metric == "L2":
+                if coupled:
+                    losses = losses + torch.mean((im_s - im_in) ** 2)
+                else:
+                    losses = losses + _per_image_mean((im_s[idx] - im_in[idx]) ** 2).sum()
+            elif att_metric == "ms-ssim":
+                if coupled:
+                    losses = losses + (1.0 - ms_ssim(im_s, im_in))
+                else:
+                    losses = losses + (1.0 - ms_ssim_per_image(im_s[idx], im_in[idx])).sum()
+            else:
+                raise ValueError(att_metric)
+        if bool((~cheap).any()):
+            idx = (~cheap).nonzero().flatten()
+            x_ = codec.g_s(P, codec.g_a(P, im_in[idx]))
+            out = codec.bound01(x_) if clamp else x_
+            if att_metric == "L2":
+                if coupled:
+                    losses = losses + (1.0 - torch.mean((output_s - out) * (output_s - out)))
+                else:
+                    d = output_s[idx] - out
+                    losses = losses + (1.0 - _per_image_mean(d * d)).sum()
+            else:
+                if coupled:
+                    losses = losses + ms_ssim(out, output_s)
+                else:
+                    losses = losses + ms_ssim_per_image(out, output_s[idx]).sum()
+        if record is not None:
+            record.append({"loss_i": li_b.detach().clone(), "cheap": cheap.clone(),
+                           "lr": opt.param_groups[0]["lr"]})
+        opt.zero_grad()
+        losses.backward()
+        opt.step()
+        if i % max(steps // 3, 1) == 0:
+            sch.step()
+    im_in = im_in.detach()
+    ev = eval_batch(P, im_in, im_s, output_s, model, clamp, adv=False, msssim=eval_msssim)
+    return SimpleNamespace(im_adv=ev.im, output_adv=ev.out, output_s=output_s, bpp_ori=bpp_ori,
+                           bpp=ev.bpp, eval=ev, noise=noise.detach(), im_in=im_in)
+
+
+def ifgsm(P, im_s, steps=10, epsilon=16.0, momentum=False, model="hyper"):
+    """attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438) without random start, per image."""
+    with torch.no_grad():
+        res = codec.forward(P, im_s, model)
+        output_s = torch.clamp(res["x_hat"], 0.0, 1.0)
+    eps = epsilon / 255.0
+    im_adv = im_s.detach().clone().requires_grad_(True)
+    g = torch.zeros_like(im_s)
+    alpha = eps / steps
+    for _ in range(steps):
+        out = codec.g_s(P, codec.g_a(P, im_adv))
+        d = output_s - out
+        loss = _per_image_mean(d * d).sum()
+        grad, = torch.autograd.grad(loss, im_adv)
+        with torch.no_grad():
+            if momentum:
+                l1 = grad.abs().flatten(1).sum(1).view(-1, 1, 1, 1)
+                g = 1.0 * g + grad / l1
+                nxt = torch.clamp(im_adv + alpha * torch.sign(g), 0, 1)
+            else:
+                nxt = im_adv + eps / steps * torch.sign(grad)
+            nxt = torch.where(nxt > im_s + eps, im_s + eps, nxt)
+            nxt = torch.where(nxt < im_s - eps, im_s - eps, nxt)
+        im_adv = nxt.detach().requires_grad_(True)
+    return im_adv.detach(), output_s
+
+
+def rd_loss(out, target, metric="mse", lmbda=0.0067):
+    """train.RateDistortionLoss.forward(training=True) (train.py:52-96)."""
+    N, _, H, W = target.shape
+    num_pixels = N * H * W
+    bpp = 0.0
+    for lik in out["likelihoods"].values():
+        lik = torch.clamp(lik, min=1.0 / 65536)
+        bpp = bpp + torch.log(lik).sum() / (-math.log(2) * num_pixels)
+    if metric == "mse":
+        d = torch.mean((out["x_hat"] - target) ** 2)
+        loss = lmbda * 255 ** 2 * d + bpp
+    elif metric == "ms-ssim":
+        d = ms_ssim(out["x_hat"], target, data_range=1.0)
+        loss = lmbda * (1 - d) + bpp
+    else:
+        raise ValueError(metric)
+    return {"loss": loss, "bpp_loss": bpp, "distortion_loss": d}
