@@ -1,0 +1,89 @@
+"""ctypes binding of libica_hip.so — the C-ABI boundary (include/ica_hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) and
+travels with the repo.  There is NO fallback: if the library is missing or a
+call returns non-zero, this raises.  torch must be imported first so that the
+HIP runtime torch bundles (soname libamdhip64.so.7) is the one the library
+binds to (single runtime, shared streams).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ICA_HIP_LIB", os.path.join(_HERE, "libica_hip.so"))
+
+_p = C.c_void_p
+_i = C.c_int
+_l = C.c_long
+_f = C.c_float
+_sz = C.c_size_t
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+_SIGS = {
+    "ica_conv_it": [_i],
+    "ica_pack_conv_weight_size": [_i, _i, _i, _i],
+    "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _p],
+    "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
+    "ica_conv_down": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
+    "ica_conv_up": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
+    "ica_elem_blocks_per_image": [],
+    "ica_nchw_to_nc4": [_p, _p, _i, _i, _i, _i, _p],
+    "ica_nc4_to_nchw": [_p, _p, _i, _i, _i, _i, _p],
+    "ica_reduce_rows": [_p, _p, _i, _i, _f, _p],
+    "ica_attack_prologue": [_p, _p, _p, _p, _i, _i, _i, _f, _p],
+    "ica_attack_loss": [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _p],
+    "ica_attack_adam": [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _f, _f, _p, _p],
+    "ica_ifgsm_step": [_p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _i, _p],
+    "ica_l1_partial": [_p, _p, _i, _i, _i, _p],
+    "ica_gc_likelihood": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
+    "ica_eb_likelihood": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
+    "ica_pack_eb": [_p, _p, _p, _i, _p],
+    "ica_abs": [_p, _p, _l, _p],
+    "ica_clamp01": [_p, _p, _l, _p],
+    "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],
+}
+_RESTYPES = {"ica_pack_conv_weight_size": _sz}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes library; raises if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libica_hip.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+                "There is no CPU/PyTorch fallback for the hot path.")
+        L = C.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, _i)
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -1,0 +1,573 @@
+// Implicit-GEMM convolutions for the Balle2018 analysis/synthesis transforms on
+// CDNA4 fp32 MFMA (v_mfma_f32_32x32x2_f32), with fused GDN/IGDN epilogues.
+//
+// Replaces (reference): the nn.Conv2d / nn.ConvTranspose2d layers built by
+// anchors/utils.py:112-130 (conv k5 s2 p2, deconv k5 s2 p2 op1, and the k3 s1
+// convs of h_a/h_s), their autograd input-gradients, and the GDN/IGDN layers of
+// utils/ops.py:58-97 (== compressai.layers.GDN) fused into the producing conv.
+//
+// GEMM orientation: D[co][px] = sum_k W[co][k] * X[k][px].  Output channels are
+// the MFMA rows (4 accumulator tiles = 128 channels per wave), pixels the MFMA
+// columns (32 per wave).  Because a wave owns ALL channels of its pixels, the
+// GDN normaliser  n = beta' + gamma' x^2  is a second in-register MFMA GEMM over
+// the accumulator rows (no LDS transpose), and GDN backward
+// u = gamma'^T (g x dS/dn) likewise.
+//
+//   conv_down : stride-S conv, KS x KS, pad KS/2.  Block = 4 waves x 32 px
+//               (TH x TW output tile), all (IT*32) channels of a channel block.
+//               K loop = channel chunks (LDS patch, CC channels) x taps.
+//   conv_up   : transposed conv k5 s2 p2 op1, decomposed into the 4 output
+//               parity classes (9/6/6/4 taps).  Block = 8x32 output pixels
+//               (4x16 per class); the whole-Cin input patch lives in LDS; each
+//               wave runs two class tiles paired 9+4 / 6+6 for balance.
+#include "ica_common.h"
+
+enum {
+  EPI_BIAS = 0,      // y = acc + bias
+  EPI_RELU = 1,      // y = relu(acc + bias)
+  EPI_GDN = 2,       // x = acc + bias; y = x * rsqrt(beta' + gamma' x^2)
+  EPI_IGDN = 3,      // x = acc + bias; y = x * sqrt(beta' + gamma' x^2)
+  EPI_GDN_BWD = 4,   // acc = dL/dy of a GDN; emit dL/dx  (needs saved x, s)
+  EPI_IGDN_BWD = 5,  // same for IGDN
+};
+
+struct ConvParams {
+  const float* x;     // input  nChw4c [N][ceil(Cin/4)][Hin][Win][4]
+  float* y;           // output nChw4c [N][ceil(Cout/4)][Hout][Wout][4]
+  const float* wp;    // packed weight fragments (ica_pack_conv_weight)
+  const float* bias;  // [Cout] or null
+  const float* gp;    // packed gamma' fragments (fwd: gamma', bwd: gamma'^T)
+  const float* beta;  // beta' [Cout] (fwd GDN epilogues)
+  float* save_x;      // fwd GDN: pre-normalisation activation (optional)
+  float* save_s;      // fwd GDN: s = rsqrt(n) | sqrt(n)           (optional)
+  const float* in_x;  // bwd GDN: saved x
+  const float* in_s;  // bwd GDN: saved s
+  int N, Cin, Hin, Win, Cout, Hout, Wout;
+};
+
+// --------------------------------------------------------------------------
+// Epilogue: acc[it] holds channels co_base + it*32 + acc_row(r,h) of pixel
+// (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
+// float4 of channel group c4 = co_base/4 + it*8 + 2g + h.
+// --------------------------------------------------------------------------
+template <int IT, int EPI>
+ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
+                           bool valid, int co_base) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int C4o = (p.Cout + 3) >> 2;
+  const size_t plane = (size_t)p.Hout * p.Wout;
+  const size_t pix = valid ? ((size_t)oy * p.Wout + ox) : 0;
+  auto off = [&](int c4) -> size_t { return (((size_t)n * C4o + c4) * plane + pix) * 4; };
+
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c0 = co_base + it * 32 + 8 * g + 4 * h;
+        if (c0 >= p.Cout) continue;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = acc[it][4 * g + e];
+          if (c0 + e < p.Cout) {
+            if (p.bias) t += p.bias[c0 + e];
+          } else {
+            t = 0.f;
+          }
+          if constexpr (EPI == EPI_RELU) t = fmaxf(t, 0.f);
+          v[e] = t;
+        }
+        if (valid) st4(p.y + off(c0 >> 2), v);
+      }
+    }
+  } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
+    // requires IT*32 == Cout, co_base == 0
+    f32x16 nacc[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = it * 32 + acc_row(r, h);
+        acc[it][r] += p.bias ? p.bias[c] : 0.f;
+        nacc[it][r] = p.beta[c];
+      }
+    }
+    if (p.save_x && valid) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          st4(p.save_x + off(it * 8 + 2 * g + h),
+              f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+    }
+    // n[c][px] = beta'[c] + sum_co gamma'[c][co] x[co][px]^2  (MFMA over accumulator rows)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+#pragma unroll
+      for (int ct = 0; ct < IT; ++ct) {
+        const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
+        const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+        const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                              g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float xv = acc[it][r];
+          nacc[ct] = mfma32(ga[r], xv * xv, nacc[ct]);
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float nv = nacc[it][r];
+        const float s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
+        nacc[it][r] = s;
+        acc[it][r] = acc[it][r] * s;
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const size_t o = off(it * 8 + 2 * g + h);
+          st4(p.y + o, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+          if (p.save_s)
+            st4(p.save_s + o, f32x4{nacc[it][4 * g], nacc[it][4 * g + 1], nacc[it][4 * g + 2], nacc[it][4 * g + 3]});
+        }
+    }
+  } else {  // EPI_GDN_BWD / EPI_IGDN_BWD, requires IT*32 == Cout
+    // t = (g * x) * dS/dn ; GDN: dS/dn = -0.5 s^3 ; IGDN: dS/dn = 0.5 / s.
+    // acc becomes g*s (first term of dx); x is re-read (L2-hot) for 2*x*u.
+    f32x16 tt[IT], uacc[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 xv = {0.f, 0.f, 0.f, 0.f}, sv = {1.f, 1.f, 1.f, 1.f};
+        if (valid) {
+          const size_t o = off(it * 8 + 2 * g + h);
+          xv = ld4(p.in_x + o);
+          sv = ld4(p.in_s + o);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          const float gx = acc[it][r] * xv[e];
+          const float s = sv[e];
+          tt[it][r] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
+          acc[it][r] = acc[it][r] * s;
+          uacc[it][r] = 0.f;
+        }
+      }
+    // u[j][px] = sum_c gamma'[c][j] t[c][px]
+#pragma unroll
+    for (int ct = 0; ct < IT; ++ct) {
+#pragma unroll
+      for (int jt = 0; jt < IT; ++jt) {
+        const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
+        const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+        const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                              g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+#pragma unroll
+        for (int r = 0; r < 16; ++r) uacc[jt] = mfma32(ga[r], tt[ct][r], uacc[jt]);
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const size_t o = off(it * 8 + 2 * g + h);
+          const f32x4 xv = ld4(p.in_x + o);
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            v[e] = acc[it][r] + 2.0f * xv[e] * uacc[it][r];
+          }
+          st4(p.y + o, v);
+        }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// conv_down: stride-S KSxKS conv, pad KS/2.  Weight fragments packed as
+// [cb][chunk][tap][it][lane][KH]  with  o = cb*IT*32 + it*32 + (lane&31),
+// c = chunk*CC + (lane>>5)*KH + s.
+// --------------------------------------------------------------------------
+template <int KS, int S, int IT, int CC, int TW, int EPI>
+__global__ __launch_bounds__(256) void conv_down_kernel(ConvParams p) {
+  constexpr int TH = 128 / TW;
+  constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
+  constexpr int NQ = CC / 4, KH = CC / 2, PLANE = PR * PC, PAD = KS / 2;
+  constexpr int WSTEP = IT * 64 * KH;  // floats per (chunk, tap)
+  __shared__ f32x4 patch[NQ * PLANE];
+
+  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int cb = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int pl = wave * 32 + j, oyl = pl / TW, oxl = pl % TW;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int Cin4 = (p.Cin + 3) >> 2;
+  const int nch = (Cin4 * 4 + CC - 1) / CC;
+
+  f32x16 acc[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+
+  const float* wcb = p.wp + (size_t)cb * nch * KS * KS * WSTEP + (size_t)lane * KH;
+  const int lbase = (S * oyl) * PC + S * oxl;
+
+  for (int ch = 0; ch < nch; ++ch) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < NQ * PLANE; e += 256) {
+      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+      const int c4 = ch * NQ + q, iy = iy0 + pr, ix = ix0 + pc;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win)
+        v = ld4(p.x + ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4);
+      patch[e] = v;
+    }
+    __syncthreads();
+    const float* wch = wcb + (size_t)ch * KS * KS * WSTEP;
+#pragma unroll
+    for (int tap = 0; tap < KS * KS; ++tap) {
+      const int ky = tap / KS, kx = tap % KS;
+      float b[KH];
+      if constexpr (CC == 16) {
+        const f32x4 v0 = patch[(2 * h) * PLANE + lbase + ky * PC + kx];
+        const f32x4 v1 = patch[(2 * h + 1) * PLANE + lbase + ky * PC + kx];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          b[e] = v0[e];
+          b[4 + e] = v1[e];
+        }
+      } else {  // CC == 4
+        const float* pf = reinterpret_cast<const float*>(&patch[lbase + ky * PC + kx]) + 2 * h;
+        const f32x2 v = *reinterpret_cast<const f32x2*>(pf);
+        b[0] = v[0];
+        b[1] = v[1];
+      }
+      const float* wt = wch + (size_t)tap * WSTEP;
+      float a[IT][KH];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        if constexpr (KH == 8) {
+          const f32x4 w0 = ld4(wt + it * 64 * KH), w1 = ld4(wt + it * 64 * KH + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[it][e] = w0[e];
+            a[it][4 + e] = w1[e];
+          }
+        } else {
+          const f32x2 w0 = *reinterpret_cast<const f32x2*>(wt + it * 64 * KH);
+          a[it][0] = w0[0];
+          a[it][1] = w0[1];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KH; ++s)
+#pragma unroll
+        for (int it = 0; it < IT; ++it) acc[it] = mfma32(a[it][s], b[s], acc[it]);
+    }
+  }
+  const int oy = oy0 + oyl, ox = ox0 + oxl;
+  conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+}
+
+// --------------------------------------------------------------------------
+// conv_up: ConvTranspose2d k5 s2 p2 op1 (Hout = 2 Hin).  Output pixel
+// y = 2a + PY uses taps ky = PY (mod 2) at input row iy = a + (PY + 2 - ky)/2.
+// Weight fragments packed [cb][tap][chunk][it][lane][8] (CC = 16).
+// --------------------------------------------------------------------------
+constexpr int UP_TH = 4, UP_TW = 16, UP_PR = UP_TH + 2, UP_PC = UP_TW + 2, UP_PLANE = UP_PR * UP_PC;
+
+template <int PY, int PX, int IT, int EPI>
+ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
+                           int nch) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int a_rel = jt * 2 + (j >> 4), b_rel = j & 15;
+  constexpr int WSTEP = IT * 64 * 8;
+  const float* wl = p.wp + (size_t)cb * 25 * nch * WSTEP + (size_t)lane * 8;
+  f32x16 acc[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+#pragma unroll
+  for (int ky = PY; ky < 5; ky += 2) {
+#pragma unroll
+    for (int kx = PX; kx < 5; kx += 2) {
+      const int pr = a_rel + 1 + (PY + 2 - ky) / 2, pc = b_rel + 1 + (PX + 2 - kx) / 2;
+      const f32x4* pp = patch + (2 * h) * UP_PLANE + pr * UP_PC + pc;
+      const float* wt = wl + (size_t)(ky * 5 + kx) * nch * WSTEP;
+
+      for (int ch = 0; ch < nch; ++ch) {
+        const f32x4 v0 = pp[(4 * ch) * UP_PLANE], v1 = pp[(4 * ch + 1) * UP_PLANE];
+        const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        float a[IT][8];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          const f32x4 w0 = ld4(wt + (size_t)ch * WSTEP + it * 512), w1 = ld4(wt + (size_t)ch * WSTEP + it * 512 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[it][e] = w0[e];
+            a[it][4 + e] = w1[e];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+          for (int it = 0; it < IT; ++it) acc[it] = mfma32(a[it][s], b[s], acc[it]);
+      }
+    }
+  }
+  const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
+  conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+}
+
+template <int IT, int EPI>
+__global__ __launch_bounds__(256) void conv_up_kernel(ConvParams p) {
+  extern __shared__ f32x4 patch[];  // [Cin4][UP_PR][UP_PC]
+  const int Hh = p.Hin, Wh = p.Win;
+  const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UP_TH - 1) / UP_TH;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int cb = blockIdx.y;
+  const int a0 = ty * UP_TH, b0 = tx * UP_TW;
+  const int Cin4 = p.Cin >> 2;  // Cin % 16 == 0 enforced by host
+  const int total = Cin4 * UP_PLANE;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int q = e / UP_PLANE, rem = e - q * UP_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
+    const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win)
+      v = ld4(p.x + ((((size_t)n * Cin4 + q) * p.Hin + iy) * p.Win + ix) * 4);
+    patch[e] = v;
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int jt = wave & 1, nch = p.Cin / 16;
+  if (wave < 2) {
+    conv_up_class<0, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<1, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+  } else {
+    conv_up_class<0, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<1, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+  }
+}
+
+// --------------------------------------------------------------------------
+// Weight / GDN-parameter packing
+// --------------------------------------------------------------------------
+// dst fragment (cb, outer, inner, it, lane, s) with
+//   order 0 (down): outer = chunk, inner = tap ; order 1 (up): outer = tap, inner = chunk
+//   o = cb*IT*32 + it*32 + (lane&31) ; c = chunk*CC + (lane>>5)*KH + s
+// value = w[o*so + c*sc + ky*KS + kx]  (0 outside O x C)
+__global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict__ dst, int O, int C, int KS,
+                                 long so, long sc, int IT, int CC, int order, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int KH = CC / 2, KK = KS * KS;
+  const int C4 = (C + 3) / 4, nch = (C4 * 4 + CC - 1) / CC;
+  long t = i;
+  const int s = t % KH; t /= KH;
+  const int lane = t % 64; t /= 64;
+  const int it = t % IT; t /= IT;
+  int inner, outer;
+  if (order == 0) { inner = t % KK; t /= KK; outer = t % nch; t /= nch; }
+  else { inner = t % nch; t /= nch; outer = t % KK; t /= KK; }
+  const int cb = (int)t;
+  const int chunk = order == 0 ? outer : inner;
+  const int tap = order == 0 ? inner : outer;
+  const int o = cb * IT * 32 + it * 32 + (lane & 31);
+  const int c = chunk * CC + (lane >> 5) * KH + s;
+  float v = 0.f;
+  if (o < O && c < C) v = w[o * so + c * sc + (tap / KS) * KS + (tap % KS)];
+  dst[i] = v;
+}
+
+// gamma' = max(gamma, 2^-18)^2 - 2^-36 ; beta' = max(beta, bound)^2 - 2^-36
+// (NonNegativeParametrizer; utils/ops.py:83-89).  Packed fragment
+// G[a][b][lane][r] = M[a*32 + (lane&31)][b*32 + acc_row(r, lane>>5)],
+// M = gamma' (transpose == 0) or gamma'^T (transpose == 1).
+__global__ void pack_gdn_kernel(const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ gp,
+                                float* __restrict__ beta_eff, int C, int transpose, float beta_bound) {
+  const int T = C / 32;
+  const long total = (long)T * T * 64 * 16;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const float ped = 1.4551915228366852e-11f;  // 2^-36
+  const float gbound = 3.814697265625e-06f;   // 2^-18
+  if (i < total) {
+    long t = i;
+    const int r = t % 16; t /= 16;
+    const int lane = t % 64; t /= 64;
+    const int b = t % T; t /= T;
+    const int a = (int)t;
+    const int row = a * 32 + (lane & 31), col = b * 32 + acc_row(r, lane >> 5);
+    const int gi = transpose ? (col * C + row) : (row * C + col);
+    const float g = fmaxf(gamma[gi], gbound);
+    gp[i] = fsub_rn(fmul_rn(g, g), ped);
+  }
+  if (i < C) {
+    const float bb = fmaxf(beta[i], beta_bound);
+    beta_eff[i] = fsub_rn(fmul_rn(bb, bb), ped);
+  }
+}
+
+// --------------------------------------------------------------------------
+// Host launchers (C ABI)
+// --------------------------------------------------------------------------
+template <int KS, int S, int IT, int CC, int TW, int EPI>
+static int launch_down(const ConvParams& p, hipStream_t st) {
+  constexpr int TH = 128 / TW;
+  const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
+  dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
+  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI>), grid, dim3(256), 0, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int KS, int S, int IT, int CC, int EPI>
+static int pick_tw_down(const ConvParams& p, hipStream_t st) {
+  if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<KS, S, IT, CC, 32, EPI>(p, st);
+  return launch_down<KS, S, IT, CC, 16, EPI>(p, st);
+}
+
+template <int KS, int S, int IT, int EPI>
+static int pick_cc_down(const ConvParams& p, hipStream_t st) {
+  if (p.Cin <= 4) return pick_tw_down<KS, S, IT, 4, EPI>(p, st);
+  if (p.Cin % 16 != 0) return -2;
+  return pick_tw_down<KS, S, IT, 16, EPI>(p, st);
+}
+
+template <int KS, int S, int EPI>
+static int pick_it_down(const ConvParams& p, int it, hipStream_t st) {
+  switch (it) {
+    case 1: return pick_cc_down<KS, S, 1, EPI>(p, st);
+    case 3: return pick_cc_down<KS, S, 3, EPI>(p, st);
+    case 4: return pick_cc_down<KS, S, 4, EPI>(p, st);
+    default: return -3;
+  }
+}
+
+template <int KS, int S>
+static int pick_epi_down(const ConvParams& p, int it, int epi, hipStream_t st) {
+  switch (epi) {
+    case EPI_BIAS: return pick_it_down<KS, S, EPI_BIAS>(p, it, st);
+    case EPI_RELU: return pick_it_down<KS, S, EPI_RELU>(p, it, st);
+    case EPI_GDN: return it == 4 ? pick_cc_down<KS, S, 4, EPI_GDN>(p, st) : -4;
+    case EPI_IGDN: return it == 4 ? pick_cc_down<KS, S, 4, EPI_IGDN>(p, st) : -4;
+    case EPI_GDN_BWD: return it == 4 ? pick_cc_down<KS, S, 4, EPI_GDN_BWD>(p, st) : -4;
+    case EPI_IGDN_BWD: return it == 4 ? pick_cc_down<KS, S, 4, EPI_IGDN_BWD>(p, st) : -4;
+    default: return -5;
+  }
+}
+
+template <int IT, int EPI>
+static int launch_up(const ConvParams& p, hipStream_t st) {
+  if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
+  const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
+  dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
+  const size_t lds = (size_t)(p.Cin / 4) * UP_PLANE * sizeof(f32x4);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<IT, EPI>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_up_kernel<IT, EPI>), grid, dim3(256), lds, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+static int pick_up(const ConvParams& p, int it, int epi, hipStream_t st) {
+  if (it == 1) {
+    if (epi == EPI_BIAS) return launch_up<1, EPI_BIAS>(p, st);
+    if (epi == EPI_RELU) return launch_up<1, EPI_RELU>(p, st);
+    return -4;
+  }
+  if (it == 4) {
+    switch (epi) {
+      case EPI_BIAS: return launch_up<4, EPI_BIAS>(p, st);
+      case EPI_RELU: return launch_up<4, EPI_RELU>(p, st);
+      case EPI_GDN: return launch_up<4, EPI_GDN>(p, st);
+      case EPI_IGDN: return launch_up<4, EPI_IGDN>(p, st);
+      case EPI_GDN_BWD: return launch_up<4, EPI_GDN_BWD>(p, st);
+      case EPI_IGDN_BWD: return launch_up<4, EPI_IGDN_BWD>(p, st);
+      default: return -5;
+    }
+  }
+  return -3;
+}
+
+extern "C" {
+
+// Channel tile (IT = number of 32-channel MFMA row tiles per wave) the conv
+// launchers use for a given output-channel count; the packer must agree.
+int ica_conv_it(int cout) {
+  if (cout <= 32) return 1;
+  if (cout % 128 == 0) return 4;
+  if (cout % 96 == 0) return 3;
+  return 4;
+}
+
+size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC) {
+  const int IT = ica_conv_it(O);
+  const int ncb = (O + IT * 32 - 1) / (IT * 32);
+  const int C4 = (C + 3) / 4, nch = (C4 * 4 + CC - 1) / CC;
+  return (size_t)ncb * nch * KS * KS * IT * 64 * (CC / 2);
+}
+
+int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long so, long sc, int CC, int order,
+                         hipStream_t st) {
+  const int IT = ica_conv_it(O);
+  const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC);
+  hipLaunchKernelGGL(pack_conv_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc, IT, CC,
+                     order, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_eff, int C, int transpose,
+                 float beta_bound, hipStream_t st) {
+  if (C % 32 != 0) return -2;
+  const long total = (long)(C / 32) * (C / 32) * 64 * 16;
+  hipLaunchKernelGGL(pack_gdn_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gamma, beta, gp, beta_eff, C,
+                     transpose, beta_bound);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                  int Cout, int Hout, int Wout, int KS, int S, int epi, const float* gp, const float* beta,
+                  float* save_x, float* save_s, const float* in_x, const float* in_s, hipStream_t st) {
+  ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout};
+  const int it = ica_conv_it(Cout);
+  if (epi >= EPI_GDN && Cout != it * 32) return -4;
+  if (KS == 5 && S == 2) return pick_epi_down<5, 2>(p, it, epi, st);
+  if (KS == 3 && S == 1) return pick_epi_down<3, 1>(p, it, epi, st);
+  return -6;
+}
+
+int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                int Cout, int Hout, int Wout, int epi, const float* gp, const float* beta, float* save_x,
+                float* save_s, const float* in_x, const float* in_s, hipStream_t st) {
+  ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout};
+  const int it = ica_conv_it(Cout);
+  if (epi >= EPI_GDN && Cout != it * 32) return -4;
+  return pick_up(p, it, epi, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,237 @@
+"""Typed host wrappers over the C ABI (torch tensors in, torch tensors out).
+
+Internal activation layout is nChw4c, stored as a torch tensor of shape
+[N, ceil(C/4), H, W, 4] (fp32, contiguous); the logical channel count travels
+with it.  All launches go on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import call, lib, ptr, stream
+
+EPI_BIAS, EPI_RELU, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD = range(6)
+ORDER_DOWN, ORDER_UP = 0, 1
+GDN_BETA_BOUND = float((1e-6 + 2.0 ** -36) ** 0.5)  # NonNegativeParametrizer bound (utils/ops.py:67)
+
+
+def _dev_check(t: torch.Tensor, name="tensor"):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a HIP device tensor (no CPU fallback on the hot path)")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+def c4(C: int) -> int:
+    return (C + 3) // 4
+
+
+def empty_nc4(N, C, H, W, device):
+    return torch.empty((N, c4(C), H, W, 4), dtype=torch.float32, device=device)
+
+
+def to_nc4(x: torch.Tensor) -> torch.Tensor:
+    x = x.contiguous()
+    _dev_check(x, "x")
+    N, C, H, W = x.shape
+    y = empty_nc4(N, C, H, W, x.device)
+    call("ica_nchw_to_nc4", ptr(x), ptr(y), N, C, H, W, stream())
+    return y
+
+
+def from_nc4(x4: torch.Tensor, C: int) -> torch.Tensor:
+    _dev_check(x4, "x4")
+    N, _, H, W, _ = x4.shape
+    y = torch.empty((N, C, H, W), dtype=torch.float32, device=x4.device)
+    call("ica_nc4_to_nchw", ptr(x4), ptr(y), N, C, H, W, stream())
+    return y
+
+
+# --------------------------------------------------------------------------- #
+# Weight packing
+# --------------------------------------------------------------------------- #
+def pack_conv(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order: int, CC: int) -> torch.Tensor:
+    """Pack a conv weight viewed as W[o][c][ky][kx] (strides so, sc; k contiguous)."""
+    w = w.detach().contiguous()
+    _dev_check(w, "weight")
+    n = int(lib().ica_pack_conv_weight_size(O, Cc, KS, CC))
+    dst = torch.empty(n, dtype=torch.float32, device=w.device)
+    call("ica_pack_conv_weight", ptr(w), ptr(dst), O, Cc, KS, so, sc, CC, order, stream())
+    return dst
+
+
+def conv_cc(Cin: int) -> int:
+    return 4 if Cin <= 4 else 16
+
+
+class PackedConv:
+    """Packed fragments for one conv layer, for both its forward and its dgrad.
+
+    kind 'conv'   : nn.Conv2d weight [Cout][Cin][k][k]   fwd = conv_down, dgrad = conv_up
+    kind 'deconv' : nn.ConvTranspose2d weight [Cin][Cout][k][k]  fwd = conv_up, dgrad = conv_down
+    """
+
+    def __init__(self, weight: torch.Tensor, bias, kind: str, stride: int):
+        self.kind = kind
+        self.stride = stride
+        self.KS = weight.shape[-1]
+        KK = self.KS * self.KS
+        if kind == "conv":
+            self.Cout, self.Cin = weight.shape[0], weight.shape[1]
+            # forward: o = co, c = ci
+            self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
+                                 conv_cc(self.Cin))
+            # dgrad (conv_up): o = ci, c = co   (only k5 s2 layers have a dgrad path)
+            self.bwd = None
+            if self.KS == 5 and stride == 2 and self.Cout % 16 == 0:
+                self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16)
+        elif kind == "deconv":
+            self.Cin, self.Cout = weight.shape[0], weight.shape[1]
+            # forward (conv_up): o = co, c = ci
+            self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16)
+            # dgrad (conv_down, stride 2): o = ci, c = co
+            self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,
+                                 conv_cc(self.Cout))
+        else:
+            raise ValueError(kind)
+        self.bias = None if bias is None else bias.detach().contiguous()
+
+
+class PackedGDN:
+    def __init__(self, beta: torch.Tensor, gamma: torch.Tensor):
+        C = beta.shape[0]
+        self.C = C
+        T = C // 32
+        dev = beta.device
+        beta = beta.detach().contiguous()
+        gamma = gamma.detach().reshape(C, C).contiguous()
+        self.gp = torch.empty(T * T * 64 * 16, device=dev)
+        self.gpT = torch.empty(T * T * 64 * 16, device=dev)
+        self.beta = torch.empty(C, device=dev)
+        call("ica_pack_gdn", ptr(gamma), ptr(beta), ptr(self.gp), ptr(self.beta), C, 0, GDN_BETA_BOUND, stream())
+        call("ica_pack_gdn", ptr(gamma), ptr(beta), ptr(self.gpT), ptr(self.beta), C, 1, GDN_BETA_BOUND, stream())
+
+
+# --------------------------------------------------------------------------- #
+# Convolutions
+# --------------------------------------------------------------------------- #
+def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False,
+              saved=None, out=None):
+    """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s)."""
+    N, _, H, W, _ = x4.shape
+    Ho = (H + 2 * (KS // 2) - KS) // S + 1
+    Wo = (W + 2 * (KS // 2) - KS) // S + 1
+    y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
+    sx = ss = None
+    if save and epi in (EPI_GDN, EPI_IGDN):
+        sx = empty_nc4(N, Cout, Ho, Wo, x4.device)
+        ss = empty_nc4(N, Cout, Ho, Wo, x4.device)
+    in_x = in_s = None
+    if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
+        in_x, in_s = saved
+    call("ica_conv_down", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, KS, S, epi,
+         ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
+         ptr(None if gdn is None else gdn.beta), ptr(sx), ptr(ss), ptr(in_x), ptr(in_s), stream())
+    return y, sx, ss
+
+
+def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
+            out=None):
+    """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
+    N, _, H, W, _ = x4.shape
+    Ho, Wo = 2 * H, 2 * W
+    y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
+    sx = ss = None
+    if save and epi in (EPI_GDN, EPI_IGDN):
+        sx = empty_nc4(N, Cout, Ho, Wo, x4.device)
+        ss = empty_nc4(N, Cout, Ho, Wo, x4.device)
+    in_x = in_s = None
+    if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
+        in_x, in_s = saved
+    call("ica_conv_up", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, epi,
+         ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
+         ptr(None if gdn is None else gdn.beta), ptr(sx), ptr(ss), ptr(in_x), ptr(in_s), stream())
+    return y, sx, ss
+
+
+# --------------------------------------------------------------------------- #
+# Reductions / elementwise
+# --------------------------------------------------------------------------- #
+def blocks_per_image() -> int:
+    return int(lib().ica_elem_blocks_per_image())
+
+
+def reduce_rows(part: torch.Tensor, B: int, scale: float = 1.0, out=None):
+    nblk = part.numel() // B
+    o = out if out is not None else torch.empty(B, device=part.device)
+    call("ica_reduce_rows", ptr(part), ptr(o), B, nblk, float(scale), stream())
+    return o
+
+
+def abs_(x: torch.Tensor) -> torch.Tensor:
+    y = torch.empty_like(x)
+    call("ica_abs", ptr(x), ptr(y), x.numel(), stream())
+    return y
+
+
+def clamp01(x: torch.Tensor) -> torch.Tensor:
+    y = torch.empty_like(x)
+    call("ica_clamp01", ptr(x), ptr(y), x.numel(), stream())
+    return y
+
+
+def sqdiff_mean(a: torch.Tensor, b: torch.Tensor, clamp_a=False) -> torch.Tensor:
+    """Per-image mean((clamp?(a) - b)^2) over the trailing dims (deterministic)."""
+    B = a.shape[0]
+    length = a[0].numel()
+    part = torch.empty(B * blocks_per_image(), device=a.device)
+    call("ica_sqdiff_partial", ptr(a.contiguous()), ptr(b.contiguous()), ptr(part), B, length, int(clamp_a), stream())
+    return reduce_rows(part, B, 1.0 / length)
+
+
+class PackedEB:
+    NAMES = ([f"_matrix{i}" for i in range(5)] + [f"_bias{i}" for i in range(5)]
+             + [f"_factor{i}" for i in range(4)] + ["quantiles"])
+
+    def __init__(self, tensors: dict):
+        import ctypes as C
+        ts = [tensors[n].detach().contiguous() for n in self.NAMES]
+        for t in ts:
+            _dev_check(t, "entropy_bottleneck param")
+        self.C = ts[-1].shape[0]
+        dev = ts[0].device
+        self.prm = torch.empty(self.C * 58, device=dev)
+        self.med = torch.empty(self.C, device=dev)
+        arr = (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+        self._keep = ts
+        # the host array of device pointers is consumed synchronously by the launcher
+        call("ica_pack_eb", C.cast(arr, C.c_void_p), ptr(self.prm), ptr(self.med), self.C, stream())
+
+
+def eb_likelihood(z4: torch.Tensor, C: int, eb: PackedEB, training=False, qnoise4=None):
+    """EntropyBottleneck forward on nc4 z: returns (z_hat4, lik4, per-image sum log lik)."""
+    N, _, H, W, _ = z4.shape
+    zh = torch.empty_like(z4)
+    lik = torch.empty_like(z4)
+    part = torch.empty(N * blocks_per_image(), device=z4.device)
+    call("ica_eb_likelihood", ptr(z4), ptr(eb.prm), ptr(eb.med), ptr(qnoise4), ptr(zh), ptr(lik), ptr(part), N, C, H,
+         W, int(training), stream())
+    return zh, lik, reduce_rows(part, N)
+
+
+def gc_likelihood(y4: torch.Tensor, C: int, scales4: torch.Tensor, means4=None, training=False, qnoise4=None):
+    N, _, H, W, _ = y4.shape
+    yh = torch.empty_like(y4)
+    lik = torch.empty_like(y4)
+    part = torch.empty(N * blocks_per_image(), device=y4.device)
+    call("ica_gc_likelihood", ptr(y4), ptr(scales4), ptr(means4), ptr(qnoise4), ptr(yh), ptr(lik), ptr(part), N, C,
+         H, W, int(training), stream())
+    return yh, lik, reduce_rows(part, N)
+
+
+def bits_to_bpp(sumlog: torch.Tensor, num_pixels: int) -> torch.Tensor:
+    return sumlog / (-math.log(2) * num_pixels)
