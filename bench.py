@@ -1,0 +1,202 @@
+"""Benchmark: attack-step·images/s on Balle2018-hyperprior q3, 512x768 (BASELINE.json configs[1]).
+
+One "step" = one attack_rd.attack_ iteration over the per-GPU batch: L-inf box
++ input clamp, g_a + g_s forward, loss, g_s + g_a input-gradient backward, Adam
+on the noise (attack_rd.py:506-559) — every kernel on HIP, inputs resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, weak scaling)
+
+Images shard across GPUs (each rank attacks its own images; no collective on
+the data path).  A single scalar MAX all-reduce of the elapsed time is the only
+collective.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "attack-step·images/sec, Balle2018-hyper 768×512 1001-step PGD, 1/2/4/8 GPU"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+
+
+def layer_flops(tag, N, M, H, W, B):
+    """Algorithmic FLOPs of one launch of a tagged conv kernel (2*MAC, padding not counted)."""
+    name, kind = tag.rsplit(".", 1)
+    lay = {  # (conv type, Cin, Cout, output resolution divisor, gdn channels in epilogue)
+        "g_a.0": ("down", 3, N, 2, N), "g_a.2": ("down", N, N, 4, N), "g_a.4": ("down", N, N, 8, N),
+        "g_a.6": ("down", N, M, 16, 0),
+        "g_s.0": ("up", M, N, 8, N), "g_s.2": ("up", N, N, 4, N), "g_s.4": ("up", N, N, 2, N),
+        "g_s.6": ("up", N, 3, 1, 0),
+    }[name]
+    typ, cin, cout, div, gdn = lay
+    out_px = (H // div) * (W // div)
+    conv_macs = cin * cout * 25 * out_px / (4 if typ == "up" else 1)
+    if kind == "fwd":
+        macs = conv_macs + gdn * gdn * out_px
+    else:  # dgrad: same conv MACs; GDN-bwd epilogue (one C x C GEMM) at the layer-input resolution
+        in_px = out_px * 4 if typ == "down" else out_px // 4
+        has_gdn = name not in ("g_a.0", "g_s.0")
+        macs = conv_macs + (N * N * in_px if has_gdn else 0)
+    return 2.0 * macs * B
+
+
+def step_flops(N, M, H, W, B):
+    tags = [f"{l}.{k}" for l in ("g_a.0", "g_a.2", "g_a.4", "g_a.6", "g_s.0", "g_s.2", "g_s.4", "g_s.6")
+            for k in ("fwd", "dgrad")]
+    return sum(layer_flops(t, N, M, H, W, B) for t in tags)
+
+
+def cpu_baseline(H, W, quality, seconds):
+    """The CPU oracle (PyTorch-CPU fp32 restatement, kind 'port') timed on this host:
+    one reference attack step on ONE image, with weight gradients computed as the
+    reference does (params require grad), bounded to ~`seconds` of CPU work."""
+    from oracle import codec
+    torch.set_num_threads(len(os.sched_getaffinity(0)))
+    P = codec.init_params("hyper", quality, seed=0)
+    for v in P.values():
+        v.requires_grad_(True)
+    g = torch.Generator().manual_seed(0)
+    im_s = torch.rand((1, 3, H, W), generator=g)
+    with torch.no_grad():
+        os_ = torch.clamp(codec.g_s(P, torch.round(codec.g_a(P, im_s))), 0, 1)
+    noise = torch.zeros_like(im_s).requires_grad_(True)
+    opt = torch.optim.Adam([noise], lr=0.01)
+    eps = 16 / 255.0
+
+    def one():
+        nc = codec.bound01(noise, -eps, eps)
+        im_in = codec.bound01(im_s + nc)
+        li = torch.mean((im_s - im_in) ** 2)
+        o = codec.bound01(codec.g_s(P, codec.g_a(P, im_in)))
+        loss = 1.0 - torch.mean((os_ - o) ** 2) if li <= 1e-4 else li
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    one()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        one()
+        n += 1
+        el = time.perf_counter() - t0
+        if el > seconds or n >= 50:
+            break
+    return {"value": n / el, "unit": "attack-step·images/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle attack step (fwd+bwd incl. weight grads as the reference), 1 image {W}x{H}, "
+                      f"hyper q{quality}, {n} timed steps after 1 warm-up ({el:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--width", type=int, default=768)
+    ap.add_argument("--quality", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from oracle import codec  # synthetic CompressAI-format weights (seeded), not the checker here
+    from imagecompression_adversarial_amd import hip_ops as K
+    from imagecompression_adversarial_amd.attack import AttackLoop
+    from imagecompression_adversarial_amd.engine import CodecKernels
+
+    H, W, B = args.height, args.width, args.batch
+    P = codec.init_params("hyper", args.quality, seed=0)
+    sd = {k: v.to(dev) for k, v in P.items()}
+    kern = CodecKernels(sd, "hyper")
+    N, M = kern.N, kern.M
+    gen = torch.Generator(device=dev).manual_seed(rank)
+    im_s = torch.rand((B, 3, H, W), generator=gen, device=dev)
+    loop = AttackLoop(kern, im_s, steps=1001)
+
+    for i in range(args.warmup):
+        loop.step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    K.EVENT_HOOK = {}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        loop.step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    hook, K.EVENT_HOOK = K.EVENT_HOOK, None
+    if dist:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # per-kernel average durations (HIP events on the launch stream)
+    per_tag = {tag: sum(a.elapsed_time(b) for a, b in evs) / len(evs) for tag, evs in hook.items()}
+    dom = max(per_tag, key=lambda t: per_tag[t] * len(hook[t]))
+    dom_ms = per_tag[dom]
+    dom_flops = layer_flops(dom, N, M, H, W, B)
+    achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+    traffic = None
+    tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(dom)
+        except Exception:
+            traffic = None
+    total_flops = step_flops(N, M, H, W, B)
+    ms_step = el / args.steps * 1e3
+    value = B * world * args.steps / el
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds)
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (torch.rand images, seeded CompressAI-init weights)",
+            "config": {"workload": f"attack_rd -m hyper -q {args.quality} -att_metric L2 -noise 1e-4, "
+                                   f"{B} images/GPU of {W}x{H}, steps of the 1001-step loop",
+                       "per_gpu_batch": B, "global_batch": B * world, "height": H, "width": W,
+                       "parallelism": f"image-shard x{world} (no data-path collective)"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
+            "step_tflops": round(total_flops / (ms_step * 1e-3) / 1e12, 2),
+            "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+            "per_kernel_ms": {k: round(v, 4) for k, v in sorted(per_tag.items())},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

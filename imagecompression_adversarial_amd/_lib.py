@@ -45,6 +45,15 @@ _SIGS = {
     "ica_abs": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],
+    "ica_nc4_bound_to_nchw": [_p, _p, _i, _i, _i, _i, _p],
+    "ica_bound_bwd_nc4": [_p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_msssim_blocks": [_i, _i, _i, _i],
+    "ica_msssim_level": [_p, _p, _i, _i, _i, _p, _i, _i, _f, _f, _p, _p, _p, _p, _p],
+    "ica_msssim_level_bwd": [_p, _p, _p, _i, _i, _i, _p, _i, _i, _p, _p, _p],
+    "ica_msssim_combine": [_p, _i, _i, _i, _p, _p, _p, _p, _p],
+    "ica_avgpool2": [_p, _p, _i, _i, _i, _i, _i, _p],
+    "ica_avgpool2_bwd": [_p, _p, _i, _i, _i, _i, _i, _p],
+    "ica_scale": [_p, _l, _f, _p],
 }
 _RESTYPES = {"ica_pack_conv_weight_size": _sz}
 

@@ -1,0 +1,213 @@
+"""The attack step loops on the HIP kernels (no autograd, no host round-trips
+inside a step except the optional per-step branch census).
+
+``attack_batch`` == attack_rd.attack_ (attack_rd.py:381-575) with attack_our
+(:332-379) and self_ensemble.eval (self_ensemble.py:173-252), batched with
+PER-IMAGE semantics: image b of the batch follows exactly the trajectory a
+B == 1 reference run would (own loss_i, own branch, own Adam state).  The
+branch `loss_i > -noise` is decided ON DEVICE per image inside the Adam kernel.
+
+``ifgsm_batch`` == attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438) without
+random start (the reference default path), per image.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from . import hip_ops as K
+from . import msssim as MS
+from ._lib import call, ptr, stream
+from .engine import CodecKernels
+
+
+def _lr_table(steps, lr):
+    # replicate torch's float arithmetic: lr is multiplied by gamma at each milestone
+    out, cur, sch = [], lr, 0
+    period = max(steps // 3, 1)
+    for i in range(steps):
+        out.append(cur)
+        if i % period == 0:
+            sch += 1
+            if sch in (1, 2, 3):
+                cur = cur * 0.33
+    return out
+
+
+@dataclass
+class AttackResult:
+    im_adv: torch.Tensor          # clamp(im_in_final, 0, 1)          [B,3,H,W]
+    output_adv: torch.Tensor      # clamp(x_hat(im_adv), 0, 1)
+    output_s: torch.Tensor        # clamp(x_hat(im_s), 0, 1)
+    bpp_ori: torch.Tensor         # [B]
+    bpp: torch.Tensor             # [B]
+    mse_in: torch.Tensor          # [B]
+    mse_out: torch.Tensor         # [B]
+    msim_in: torch.Tensor | None  # [B]
+    msim_out: torch.Tensor | None
+    vi: list = field(default_factory=list)
+    vi_msim: list = field(default_factory=list)
+    noise: torch.Tensor | None = None
+    branches: list = field(default_factory=list)
+
+
+def eval_forward(kern: CodecKernels, x: torch.Tensor, clamp=True):
+    """net.eval(); net(x) -> (output_ = clamp?(x_hat) NCHW, bpp[B])."""
+    B, _, H, W = x.shape
+    res = kern.forward(K.to_nc4(x))
+    out = torch.empty_like(x)
+    call("ica_nc4_bound_to_nchw", ptr(res["x_hat4"]), ptr(out), B, H, W, int(clamp), stream())
+    return out, K.bits_to_bpp(res["sumlog"], H * W)
+
+
+def evaluate(kern, im_in, im_s, output_s, clamp=True, adv=False, msssim=True):
+    """self_ensemble.eval (self_ensemble.py:173-252), per image."""
+    im_ = K.clamp01(im_in) if clamp else im_in
+    out, bpp = eval_forward(kern, im_, clamp)
+    mse_in = K.sqdiff_mean(im_, im_s)
+    mse_out = K.sqdiff_mean(out, output_s)
+    msim_in = msim_out = None
+    if msssim:
+        msim_in = MS.ms_ssim_per_image(im_, im_s)
+        msim_out = MS.ms_ssim_per_image(out, output_s)
+    vi, vi_msim = [], []
+    mi_l, mo_l = mse_in.tolist(), mse_out.tolist()
+    si_l = msim_in.tolist() if msssim else [None] * len(mi_l)
+    so_l = msim_out.tolist() if msssim else [None] * len(mi_l)
+    for mi, mo, si, so in zip(mi_l, mo_l, si_l, so_l):
+        v = vm = None
+        if mi > 1e-20 and mo > 1e-20:
+            v = 10.0 * math.log10(mo / mi)
+            if not adv and si is not None and si < 0.9999:
+                vm = 10.0 * math.log10((1 - so) / (1 - si))
+        vi.append(v)
+        vi_msim.append(vm)
+    return im_, out, bpp, mse_in, mse_out, msim_in, msim_out, vi, vi_msim
+
+
+class AttackLoop:
+    """Holds the device state of one batched attack_rd.attack_ run."""
+
+    def __init__(self, kern: CodecKernels, im_s: torch.Tensor, steps=1001, epsilon=16.0, noise_thr=1e-4,
+                 lr=0.01, att_metric="L2", clamp=True, init_noise=None):
+        if att_metric not in ("L2", "ms-ssim"):
+            raise ValueError(f"att_metric {att_metric!r} not supported (reference: L2, ms-ssim)")
+        self.kern = kern
+        self.im_s = im_s.contiguous()
+        B, C, H, W = im_s.shape
+        assert C == 3
+        self.B, self.H, self.W = B, H, W
+        self.steps, self.eps, self.thr = steps, float(epsilon) / 255.0, float(noise_thr)
+        self.metric, self.clamp = att_metric, clamp
+        self.invN = float(1.0 / (3 * H * W))  # torch: grad / numel in fp32
+        dev = im_s.device
+        self.noise = torch.zeros_like(self.im_s) if init_noise is None else init_noise.clone().contiguous()
+        self.m = torch.zeros_like(self.im_s)
+        self.v = torch.zeros_like(self.im_s)
+        self.im_in4 = K.empty_nc4(B, 3, H, W, dev)
+        self.part = torch.empty(B * K.blocks_per_image(), device=dev)
+        self.loss_i = torch.empty(B, device=dev)
+        self.grad4 = K.empty_nc4(B, 3, H, W, dev)
+        self.branch = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.im_in = torch.empty_like(self.im_s)
+        self.lrs = _lr_table(steps, lr)
+        self.t = 0
+        # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
+        self.output_s, self.bpp_ori = eval_forward(kern, self.im_s, clamp)
+        self.output_s4 = None
+
+    def _adam_scalars(self, i):
+        t = i + 1
+        bc1 = 1 - 0.9 ** t
+        bc2 = 1 - 0.999 ** t
+        step_size = self.lrs[i] / bc1
+        return float(bc2 ** 0.5), float(-step_size)
+
+    def network_grad(self):
+        """x_hat = g_s(g_a(im_in)); grad4 = d loss_o / d im_in (nChw4c, C=3)."""
+        kern = self.kern
+        B, H, W = self.B, self.H, self.W
+        y4, sa = kern.g_a(self.im_in4, save=True)
+        xh4, ss = kern.g_s(y4, save=True)
+        del y4
+        if self.metric == "L2":
+            call("ica_attack_loss", ptr(xh4), ptr(self.output_s), ptr(self.grad4), ptr(self.part), B, H, W,
+                 self.invN, int(self.clamp), 0, stream())
+        else:
+            # loss_o = ms_ssim(out, output_s) per image (attack_rd.py:362)
+            out = torch.empty_like(self.im_s)
+            call("ica_nc4_bound_to_nchw", ptr(xh4), ptr(out), B, H, W, int(self.clamp), stream())
+            ones = torch.ones(B, device=out.device)
+            _, gout, _ = MS.ms_ssim_value_and_grad(out, self.output_s, ones)
+            call("ica_bound_bwd_nc4", ptr(xh4), ptr(gout), ptr(self.grad4), B, H, W, int(self.clamp), stream())
+        gy4 = kern.g_s_backward(self.grad4, ss)
+        del ss, xh4
+        return kern.g_a_backward(gy4, sa)
+
+    def step(self, i, record_im_in=False, census=False):
+        B, H, W = self.B, self.H, self.W
+        call("ica_attack_prologue", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
+             self.eps, stream())
+        K.reduce_rows(self.part, B, self.invN, out=self.loss_i)
+        gx4 = self.network_grad()
+        cheap_grad = None
+        if self.metric == "ms-ssim":
+            # cheap branch loss = 1 - ms_ssim(im_s, im_in): d/d im_in = -dMS/dY
+            im_in = torch.empty_like(self.im_s)
+            call("ica_nc4_bound_to_nchw", ptr(self.im_in4), ptr(im_in), B, H, W, 0, stream())
+            _, _, gY = MS.ms_ssim_value_and_grad(self.im_s, im_in, -torch.ones(B, device=im_in.device))
+            cheap_grad = gY
+        bc2s, neg_step = self._adam_scalars(i)
+        call("ica_attack_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(cheap_grad),
+             ptr(self.m), ptr(self.v), ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr,
+             self.invN, bc2s, neg_step, ptr(self.branch), stream())
+        if census:
+            return self.branch.tolist()
+        return None
+
+    def run(self, record=False):
+        branches = []
+        for i in range(self.steps):
+            br = self.step(i, record_im_in=(i == self.steps - 1), census=record)
+            if record:
+                branches.append(br)
+        return branches
+
+
+def attack_batch(kern: CodecKernels, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
+                 clamp=True, init_noise=None, eval_msssim=True, record=False) -> AttackResult:
+    loop = AttackLoop(kern, im_s, steps, epsilon, noise_thr, lr, att_metric, clamp, init_noise)
+    branches = loop.run(record=record)
+    im_, out, bpp, mse_in, mse_out, msim_in, msim_out, vi, vi_msim = evaluate(
+        kern, loop.im_in, loop.im_s, loop.output_s, clamp, adv=False, msssim=eval_msssim)
+    return AttackResult(im_adv=im_, output_adv=out, output_s=loop.output_s, bpp_ori=loop.bpp_ori, bpp=bpp,
+                        mse_in=mse_in, mse_out=mse_out, msim_in=msim_in, msim_out=msim_out, vi=vi, vi_msim=vi_msim,
+                        noise=loop.noise, branches=branches)
+
+
+def ifgsm_batch(kern: CodecKernels, im_s, steps=10, epsilon=16.0, momentum=False, clamp=True):
+    """attack_ifgsm.attack_ifgsm (no random start); returns (im_adv, output_s)."""
+    B, _, H, W = im_s.shape
+    im_s = im_s.contiguous()
+    output_s, _ = eval_forward(kern, im_s, clamp=True)
+    eps = float(epsilon) / 255.0
+    alpha = float(eps / steps)
+    x = im_s.clone()
+    gacc = torch.zeros_like(x)
+    part = torch.empty(B * K.blocks_per_image(), device=x.device)
+    grad4 = K.empty_nc4(B, 3, H, W, x.device)
+    l1 = torch.empty(B, device=x.device)
+    invN = float(1.0 / (3 * H * W))
+    for _ in range(steps):
+        y4, sa = kern.g_a(K.to_nc4(x), save=True)
+        xh4, ss = kern.g_s(y4, save=True)
+        call("ica_attack_loss", ptr(xh4), ptr(output_s), ptr(grad4), ptr(part), B, H, W, invN, 0, 1, stream())
+        gx4 = kern.g_a_backward(kern.g_s_backward(grad4, ss), sa)
+        if momentum:
+            call("ica_l1_partial", ptr(gx4), ptr(part), B, H, W, stream())
+            K.reduce_rows(part, B, 1.0, out=l1)
+        call("ica_ifgsm_step", ptr(x), ptr(im_s), ptr(gx4), ptr(gacc), ptr(l1), B, H, W, alpha, eps, int(momentum),
+             stream())
+    return x, output_s

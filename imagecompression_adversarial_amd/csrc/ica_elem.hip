@@ -416,6 +416,37 @@ __global__ void sqdiff_partial_kernel(const float* __restrict__ a, const float* 
   if (threadIdx.x == 0) part[(long)b * gridDim.x + blockIdx.x] = r;
 }
 
+// out = Up(Low(x_hat,0),1) (or x_hat) written NCHW from an nChw4c tensor with C = 3.
+__global__ void nc4_bound_to_nchw_kernel(const float* __restrict__ x4, float* __restrict__ out, long HW, int clamp) {
+  const int b = blockIdx.y;
+  for (long pix = (long)blockIdx.x * 256 + threadIdx.x; pix < HW; pix += (long)gridDim.x * 256) {
+    const f32x4 v = ld4(x4 + ((long)b * HW + pix) * 4);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[((long)b * 3 + c) * HW + pix] = clamp ? fminf(fmaxf(v[c], 0.f), 1.f) : v[c];
+  }
+}
+
+// g4 = bound01-backward(g (NCHW, dL/dout)) at x_hat4, in nChw4c (C = 3).
+__global__ void bound_bwd_nc4_kernel(const float* __restrict__ x4, const float* __restrict__ g,
+                                     float* __restrict__ g4, long HW, int clamp) {
+  const int b = blockIdx.y;
+  for (long pix = (long)blockIdx.x * 256 + threadIdx.x; pix < HW; pix += (long)gridDim.x * 256) {
+    const f32x4 v = ld4(x4 + ((long)b * HW + pix) * 4);
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float gg = g[((long)b * 3 + c) * HW + pix];
+      if (clamp) {
+        const float xh = v[c], lo = fmaxf(xh, 0.f);
+        gg = (lo <= 1.f || gg > 0.f) ? gg : gg * 0.f;
+        gg = (xh >= 0.f || gg < 0.f) ? gg : gg * 0.f;
+      }
+      o[c] = gg;
+    }
+    st4(g4 + ((long)b * HW + pix) * 4, o);
+  }
+}
+
 __global__ void clamp01_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     y[i] = fminf(fmaxf(x[i], 0.f), 1.f);
@@ -523,6 +554,20 @@ int ica_pack_eb(const float* const* params, float* prm, float* med, int C, hipSt
 
 int ica_abs(const float* x, float* y, long n, hipStream_t st) {
   hipLaunchKernelGGL(abs_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_nc4_bound_to_nchw(const float* x4, float* out, int B, int H, int W, int clamp, hipStream_t st) {
+  hipLaunchKernelGGL(nc4_bound_to_nchw_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x4, out, (long)H * W,
+                     clamp);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_bound_bwd_nc4(const float* x4, const float* g, float* g4, int B, int H, int W, int clamp, hipStream_t st) {
+  hipLaunchKernelGGL(bound_bwd_nc4_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x4, g, g4, (long)H * W,
+                     clamp);
   ICA_CHECK_LAUNCH();
   return 0;
 }

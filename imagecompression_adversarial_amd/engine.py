@@ -48,20 +48,21 @@ class CodecKernels:
         h, C, saved = x4, 3, []
         for i in range(3):
             p = self.ga[i]
-            h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.ga_gdn[i], save)
+            h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.ga_gdn[i], save,
+                                    tag=f"g_a.{2 * i}.fwd")
             saved.append((sx, ss))
             C = self.N
         p = self.ga[3]
-        y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS)
+        y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS, tag="g_a.6.fwd")
         return y, saved
 
     def g_a_backward(self, gy4, saved):
         g, C = gy4, self.M
         for i in (3, 2, 1):
             g, _, _ = K.conv_up(g, C, self.ga[i].bwd, None, self.N, K.EPI_GDN_BWD, self.ga_gdn[i - 1],
-                                saved=saved[i - 1])
+                                saved=saved[i - 1], tag=f"g_a.{2 * i}.dgrad")
             C = self.N
-        gx, _, _ = K.conv_up(g, self.N, self.ga[0].bwd, None, 3, K.EPI_BIAS)
+        gx, _, _ = K.conv_up(g, self.N, self.ga[0].bwd, None, 3, K.EPI_BIAS, tag="g_a.0.dgrad")
         return gx
 
     # ------------------------------------------------------------------ g_s
@@ -69,20 +70,21 @@ class CodecKernels:
         h, C, saved = y4, self.M, []
         for i in range(3):
             p = self.gs[i]
-            h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gs_gdn[i], save)
+            h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gs_gdn[i], save,
+                                  tag=f"g_s.{2 * i}.fwd")
             saved.append((sx, ss))
             C = self.N
         p = self.gs[3]
-        xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS)
+        xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS, tag="g_s.6.fwd")
         return xh, saved
 
     def g_s_backward(self, gx4, saved):
         g, C = gx4, 3
         for i in (3, 2, 1):
             g, _, _ = K.conv_down(g, C, self.gs[i].bwd, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gs_gdn[i - 1],
-                                  saved=saved[i - 1])
+                                  saved=saved[i - 1], tag=f"g_s.{2 * i}.dgrad")
             C = self.N
-        gy, _, _ = K.conv_down(g, self.N, self.gs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS)
+        gy, _, _ = K.conv_down(g, self.N, self.gs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS, tag="g_s.0.dgrad")
         return gy
 
     # ------------------------------------------------------------------ hyperprior

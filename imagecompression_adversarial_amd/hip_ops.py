@@ -17,6 +17,27 @@ ORDER_DOWN, ORDER_UP = 0, 1
 GDN_BETA_BOUND = float((1e-6 + 2.0 ** -36) ** 0.5)  # NonNegativeParametrizer bound (utils/ops.py:67)
 
 
+# Optional per-launch timing hook used by bench.py: {tag: [(ev0, ev1), ...]}.
+# When set, every tagged conv launch is bracketed by HIP events recorded on
+# the current stream (the stream the kernel runs on); no synchronisation.
+EVENT_HOOK = None
+
+
+def _ev_begin(tag):
+    if EVENT_HOOK is None or tag is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return (tag, e0)
+
+
+def _ev_end(h):
+    if h is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        EVENT_HOOK.setdefault(h[0], []).append((h[1], e1))
+
+
 def _dev_check(t: torch.Tensor, name="tensor"):
     if not t.is_cuda:
         raise RuntimeError(f"{name} must be a HIP device tensor (no CPU fallback on the hot path)")
@@ -120,7 +141,7 @@ class PackedGDN:
 # Convolutions
 # --------------------------------------------------------------------------- #
 def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False,
-              saved=None, out=None):
+              saved=None, out=None, tag=None):
     """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s)."""
     N, _, H, W, _ = x4.shape
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
@@ -133,14 +154,16 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     in_x = in_s = None
     if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
         in_x, in_s = saved
+    ev = _ev_begin(tag)
     call("ica_conv_down", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, KS, S, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
          ptr(None if gdn is None else gdn.beta), ptr(sx), ptr(ss), ptr(in_x), ptr(in_s), stream())
+    _ev_end(ev)
     return y, sx, ss
 
 
 def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
-            out=None):
+            out=None, tag=None):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
     Ho, Wo = 2 * H, 2 * W
@@ -152,9 +175,11 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     in_x = in_s = None
     if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
         in_x, in_s = saved
+    ev = _ev_begin(tag)
     call("ica_conv_up", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
          ptr(None if gdn is None else gdn.beta), ptr(sx), ptr(ss), ptr(in_x), ptr(in_s), stream())
+    _ev_end(ev)
     return y, sx, ss
 
 

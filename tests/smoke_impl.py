@@ -1,0 +1,34 @@
+"""One tiny attack step on cuda:0 checked against the CPU oracle (used by __graft_entry__.smoke)."""
+import torch
+
+from oracle import codec
+from oracle import attack as oatt
+
+
+def _params(device):
+    P = codec.perturb_params(codec.init_params("hyper", 3, seed=0), seed=1)
+    return P, {k: v.to(device) for k, v in P.items()}
+
+
+def run_smoke():
+    from imagecompression_adversarial_amd.attack import attack_batch
+    from imagecompression_adversarial_amd.engine import CodecKernels
+    from imagecompression_adversarial_amd import _lib
+    dev = torch.device("cuda:0")
+    P, Pd = _params(dev)
+    kern = CodecKernels(Pd, "hyper")
+    x = torch.rand((1, 3, 64, 64), generator=torch.Generator().manual_seed(7))
+    res = attack_batch(kern, x.to(dev), steps=3, eval_msssim=False)
+    ref = oatt.attack(P, x, steps=3, eval_msssim=False)
+    torch.cuda.synchronize()
+    err_s = (res.output_s.cpu() - ref.output_s).abs().max().item()
+    err_n = (res.noise.cpu() - ref.noise).abs().max().item() / max(ref.noise.abs().max().item(), 1e-30)
+    err_b = abs(res.bpp_ori.item() - ref.bpp_ori.item())
+    assert err_s < 1e-4, f"output_s mismatch {err_s}"
+    assert err_n < 1e-3, f"noise mismatch {err_n}"
+    assert err_b < 1e-3, f"bpp mismatch {err_b}"
+    print(f"smoke ok: lib={_lib.LIB_PATH} |d output_s|={err_s:.2e} rel|d noise|={err_n:.2e} |d bpp|={err_b:.2e}")
+
+
+if __name__ == "__main__":
+    run_smoke()

@@ -1,0 +1,174 @@
+"""GPU parity of the composed hot path vs the CPU oracle and the golden vectors.
+
+Tolerances (stated): fp32 chain outputs rel <= 1e-4; input gradient through
+g_a+g_s (8 conv layers + 6 GDN) rel <= 1e-3 of its max; attack trajectories:
+identical branch sequence, final noise rel <= 1e-3, im_in rel <= 1e-5;
+batch independence BIT-EXACT; L-inf box / [0,1] invariants exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import attack as oatt
+from oracle import codec
+from oracle import msssim as omsssim
+from tests.conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def rnd(shape, seed, lo=0.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g) * (hi - lo) + lo
+
+
+@pytest.fixture(scope="module")
+def hyper3():
+    from imagecompression_adversarial_amd.engine import CodecKernels
+    P = codec.perturb_params(codec.init_params("hyper", 3, seed=0), seed=1)
+    Pd = {k: v.to(DEV) for k, v in P.items()}
+    return P, CodecKernels(Pd, "hyper")
+
+
+def test_stack_fwd_dgrad_vs_golden(golden, hyper3):
+    from imagecompression_adversarial_amd import hip_ops as K
+    from imagecompression_adversarial_amd._lib import call, ptr, stream
+    P, kern = hyper3
+    xs = rnd((1, 3, 64, 64), 7)
+    xi = codec.bound01(xs + rnd((1, 3, 64, 64), 8, -0.03, 0.03)).detach()
+    y4, sa = kern.g_a(K.to_nc4(xi.to(DEV)), save=True)
+    xh4, ss = kern.g_s(y4, save=True)
+    assert rel_err(K.from_nc4(y4, 192).cpu(), golden["stack_y"]) < 1e-4
+    assert rel_err(K.from_nc4(xh4, 3).cpu(), golden["stack_xhat"]) < 1e-4
+    os_ = torch.tensor(golden["stack_output_s"]).to(DEV)
+    g4 = K.empty_nc4(1, 3, 64, 64, DEV)
+    part = torch.empty(K.blocks_per_image(), device=DEV)
+    call("ica_attack_loss", ptr(xh4), ptr(os_), ptr(g4), ptr(part), 1, 64, 64, float(1.0 / (3 * 64 * 64)), 1, 0,
+         stream())
+    mse = K.reduce_rows(part, 1, 1.0 / (3 * 64 * 64))
+    assert abs((1.0 - mse.item()) - float(golden["stack_loss"])) < 1e-6
+    gx4 = kern.g_a_backward(kern.g_s_backward(g4, ss), sa)
+    assert rel_err(K.from_nc4(gx4, 3).cpu(), golden["stack_dx"]) < 1e-3
+
+
+def test_attack_trajectory_vs_golden(golden, hyper3):
+    from imagecompression_adversarial_amd.attack import AttackLoop
+    P, kern = hyper3
+    xs = rnd((1, 3, 64, 64), 7)
+    for tag in ("traj", "traj2"):
+        loop = AttackLoop(kern, xs.to(DEV), steps=12, noise_thr=float(golden[f"{tag}_thr"]))
+        assert rel_err(loop.output_s.cpu(), golden["stack_output_s"]) < 1e-4
+        br = [loop.step(i, record_im_in=True, census=True)[0] for i in range(12)]
+        assert br == list(golden[f"{tag}_branch"])
+        assert rel_err(loop.noise.cpu(), golden[f"{tag}_noise"]) < 1e-3
+        assert rel_err(loop.im_in.cpu(), golden[f"{tag}_im_in"]) < 1e-5
+
+
+def test_attack_vs_oracle_256(hyper3):
+    """Config-1 shape (256x256), 6 steps, default -noise: result and eval metrics vs oracle."""
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = hyper3
+    x = rnd((2, 3, 256, 256), 21)
+    res = attack_batch(kern, x.to(DEV), steps=6)
+    ref = oatt.attack(P, x, steps=6)
+    assert rel_err(res.output_s.cpu(), ref.output_s) < 1e-4
+    assert rel_err(res.noise.cpu(), ref.noise) < 2e-3
+    assert rel_err(res.im_adv.cpu(), ref.im_adv) < 1e-5
+    assert torch.allclose(res.bpp_ori.cpu(), ref.bpp_ori, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(res.bpp.cpu(), ref.bpp, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(res.mse_in.cpu(), ref.eval.mse_in, rtol=1e-3, atol=1e-12)
+    assert torch.allclose(res.msim_in.cpu(), ref.eval.msim_in, rtol=0, atol=1e-5)
+    assert torch.allclose(res.msim_out.cpu(), ref.eval.msim_out, rtol=0, atol=1e-5)
+
+
+def test_batch_independence_bitexact(hyper3):
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = hyper3
+    x = rnd((3, 3, 128, 192), 31).to(DEV)
+    rb = attack_batch(kern, x, steps=4, eval_msssim=False)
+    r1 = attack_batch(kern, x[1:2].contiguous(), steps=4, eval_msssim=False)
+    assert torch.equal(rb.noise[1:2], r1.noise)
+    assert torch.equal(rb.output_adv[1:2], r1.output_adv)
+    assert torch.equal(rb.bpp[1:2], r1.bpp)
+
+
+def test_invariants(hyper3):
+    from imagecompression_adversarial_amd.attack import AttackLoop
+    P, kern = hyper3
+    x = rnd((2, 3, 128, 128), 41).to(DEV)
+    loop = AttackLoop(kern, x, steps=5, noise_thr=1e-9, lr=0.2)
+    for i in range(5):
+        loop.step(i, record_im_in=True)
+    eps = np.float32(16 / 255.0)
+    d = (loop.im_in - x).abs().max().item()
+    assert d <= eps * (1 + 1e-6)
+    assert float(loop.im_in.min()) >= 0.0 and float(loop.im_in.max()) <= 1.0
+
+
+def test_msssim_vs_oracle():
+    from imagecompression_adversarial_amd import msssim as MS
+    a = rnd((2, 3, 192, 200), 51)
+    b = torch.clamp(a + (rnd((2, 3, 192, 200), 52) - 0.5) * 0.2, 0, 1)
+    ad, bd = a.to(DEV), b.to(DEV)
+    v = MS.ms_ssim_per_image(ad, bd).cpu()
+    ref = omsssim.ms_ssim_per_image(a, b)
+    assert torch.allclose(v, ref, atol=2e-6)
+    # backward (pytorch_msssim variant)
+    br = b.clone().requires_grad_(True)
+    omsssim.ms_ssim_per_image(a, br).sum().backward()
+    _, gX, gY = MS.ms_ssim_value_and_grad(ad, bd, torch.ones(2, device=DEV))
+    assert rel_err(gY.cpu(), br.grad) < 1e-3
+    # torch_msssim variant (global mean), incl. even window at the last level (64x64 -> 4x4)
+    for shape in ((1, 3, 192, 192), (2, 3, 64, 64)):
+        a = rnd(shape, 53)
+        b = torch.clamp(a + (rnd(shape, 54) - 0.5) * 0.2, 0, 1)
+        br = b.clone().requires_grad_(True)
+        ref = omsssim.torch_msssim(a, br)
+        ref.backward()
+        val, gX, gY = MS.ms_ssim_value_and_grad(a.to(DEV), b.to(DEV), torch.ones(1, device=DEV), mode=1)
+        assert abs(val.item() - ref.item()) < 2e-6
+        assert rel_err(gY.cpu(), br.grad) < 1e-3
+
+
+def test_ms_ssim_attack_metric(hyper3):
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = hyper3
+    x = rnd((1, 3, 192, 192), 61)
+    res = attack_batch(kern, x.to(DEV), steps=3, att_metric="ms-ssim", eval_msssim=False)
+    ref = oatt.attack(P, x, steps=3, att_metric="ms-ssim", eval_msssim=False)
+    # Adam divides by sqrt(v): elements whose MS-SSIM gradient is ~eps amplify fp32
+    # ordering differences; bound the max and require 99.9% of elements tight.
+    d = (res.noise.cpu() - ref.noise).abs() / ref.noise.abs().max()
+    assert float(d.max()) < 2e-2
+    assert float((d > 1e-3).float().mean()) < 1e-3
+
+
+def test_ifgsm_vs_oracle(hyper3):
+    from imagecompression_adversarial_amd.attack import ifgsm_batch
+    P, kern = hyper3
+    x = rnd((1, 3, 64, 128), 71)
+    for momentum in (False, True):
+        xa, _ = ifgsm_batch(kern, x.to(DEV), steps=4, momentum=momentum)
+        xr, _ = oatt.ifgsm(P, x, steps=4, momentum=momentum)
+        diff = (xa.cpu() - xr).abs()
+        eps_step = (16 / 255.0) / 4
+        # sign() is discontinuous: allow a tiny fraction of elements to take the other sign
+        assert float((diff > 1e-6).float().mean()) < 1e-3
+        assert float(diff.max()) <= 2 * eps_step + 1e-6
+
+
+def test_entropy_models_vs_oracle(hyper3):
+    from imagecompression_adversarial_amd import hip_ops as K
+    P, kern = hyper3
+    z = rnd((2, 128, 4, 6), 81, -20, 20)
+    zh4, lik4, s = K.eb_likelihood(K.to_nc4(z.to(DEV)), 128, kern.eb)
+    zr, lr = codec.entropy_bottleneck(P, z)
+    assert torch.equal(K.from_nc4(zh4, 128).cpu(), zr)
+    assert rel_err(K.from_nc4(lik4, 128).cpu(), lr) < 1e-4
+    y = rnd((2, 192, 4, 6), 82, -10, 10)
+    sc = rnd((2, 192, 4, 6), 83, 0.0, 5.0)
+    yh4, ylik4, _ = K.gc_likelihood(K.to_nc4(y.to(DEV)), 192, K.to_nc4(sc.to(DEV)))
+    yr, ylr = codec.gaussian_conditional(y, sc)
+    assert torch.equal(K.from_nc4(yh4, 192).cpu(), yr)
+    assert rel_err(K.from_nc4(ylik4, 192).cpu(), ylr) < 1e-4
