@@ -60,7 +60,8 @@ def cpu_baseline(H, W, quality, seconds):
     one reference attack step on ONE image, with weight gradients computed as the
     reference does (params require grad), bounded to ~`seconds` of CPU work."""
     from oracle import codec
-    torch.set_num_threads(len(os.sched_getaffinity(0)))
+    # the box's CPU share (OMP_NUM_THREADS is set to it there); never oversubscribe
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0)))))
     P = codec.init_params("hyper", quality, seed=0)
     for v in P.values():
         v.requires_grad_(True)

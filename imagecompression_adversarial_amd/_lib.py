@@ -28,6 +28,9 @@ _SIGS = {
     "ica_pack_conv_weight_size": [_i, _i, _i, _i],
     "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
+    "ica_pack_up3_size": [_i],
+    "ica_pack_up3": [_p, _p, _i, _p],
+    "ica_conv_up3": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
     "ica_conv_down": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
     "ica_conv_up": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
     "ica_elem_blocks_per_image": [],
@@ -55,7 +58,7 @@ _SIGS = {
     "ica_avgpool2_bwd": [_p, _p, _i, _i, _i, _i, _i, _p],
     "ica_scale": [_p, _l, _f, _p],
 }
-_RESTYPES = {"ica_pack_conv_weight_size": _sz}
+_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_up3_size": _sz}
 
 _lib = None
 

@@ -369,6 +369,126 @@ __global__ __launch_bounds__(256) void conv_up_kernel(ConvParams p) {
 }
 
 // --------------------------------------------------------------------------
+// conv_up to 3 channels (g_s last deconv k5 s2 128->3, and the input-gradient
+// of g_a's first conv 3->128).  A naive class decomposition would pad the 3
+// output channels to a 32-row MFMA tile (10.7x waste).  Instead:
+//   Z[(co,ky,kx)][pixel] = sum_ci W[ci][co][ky][kx] * x[ci][pixel]   (75 x Cin dense GEMM)
+//   out[co][2a+py][2b+px] = sum_{ky=py, kx=px (mod 2)} Z[(co,ky,kx)][a+dy, b+dx]
+// The block owns an 8x32 input-pixel tile; Z is computed for its 10x34 halo
+// tile into LDS (75 x 340 floats), then each thread gathers the 12 outputs of
+// one input pixel.  Weight fragments packed [it(3)][chunk][lane][8] with row
+// o = it*32 + (lane&31) = co*25 + ky*5 + kx.
+// --------------------------------------------------------------------------
+constexpr int T3_TH = 8, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 340
+constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                            // 11
+
+__global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
+  __shared__ float zs[T3_ROWS * T3_NPX];
+  const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int a0 = ty * T3_TH, b0 = tx * T3_TW;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Cin4 = p.Cin >> 2, nch = p.Cin / 16;
+  const size_t plane = (size_t)p.Hin * p.Win;
+  for (int jt = wave; jt < T3_JT; jt += 4) {
+    const int q = jt * 32 + j;
+    const int hr = q / T3_HC, hc = q - hr * T3_HC;
+    const int iy = a0 - 1 + hr, ix = b0 - 1 + hc;
+    const bool ok = q < T3_NPX && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+    const float* xp = p.x + (((size_t)n * Cin4) * plane + (ok ? (size_t)iy * p.Win + ix : 0)) * 4;
+    f32x16 acc[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) acc[it] = f32x16{0};
+    const float* wl = p.wp + (size_t)lane * 8;
+    for (int ch = 0; ch < nch; ++ch) {
+      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        v0 = ld4(xp + (size_t)(4 * ch + 2 * h) * plane * 4);
+        v1 = ld4(xp + (size_t)(4 * ch + 2 * h + 1) * plane * 4);
+      }
+      const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      float a[3][8];
+#pragma unroll
+      for (int it = 0; it < 3; ++it) {
+        const float* wt = wl + ((size_t)it * nch + ch) * 512;
+        const f32x4 w0 = ld4(wt), w1 = ld4(wt + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[it][e] = w0[e];
+          a[it][4 + e] = w1[e];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int it = 0; it < 3; ++it) acc[it] = mfma32(a[it][s], b[s], acc[it]);
+    }
+    if (q < T3_NPX) {
+#pragma unroll
+      for (int it = 0; it < 3; ++it)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = it * 32 + acc_row(r, h);
+          if (row < T3_ROWS) zs[row * T3_NPX + q] = acc[it][r];
+        }
+    }
+  }
+  __syncthreads();
+  // gather: thread -> input pixel (a, b) of the owned tile, 4 classes x 3 channels
+  const int al = threadIdx.x / T3_TW, bl = threadIdx.x % T3_TW;
+  const int a = a0 + al, b = b0 + bl;
+  if (a >= p.Hin || b >= p.Win) return;
+  const float bias0 = p.bias ? p.bias[0] : 0.f, bias1 = p.bias ? p.bias[1] : 0.f, bias2 = p.bias ? p.bias[2] : 0.f;
+#pragma unroll
+  for (int py = 0; py < 2; ++py) {
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+#pragma unroll
+      for (int ky = py; ky < 5; ky += 2) {
+#pragma unroll
+        for (int kx = px; kx < 5; kx += 2) {
+          const int dy = (py + 2 - ky) / 2, dx = (px + 2 - kx) / 2;
+          const int q = (al + 1 + dy) * T3_HC + (bl + 1 + dx);
+          const int tap = ky * 5 + kx;
+          o0 += zs[(0 * 25 + tap) * T3_NPX + q];
+          o1 += zs[(1 * 25 + tap) * T3_NPX + q];
+          o2 += zs[(2 * 25 + tap) * T3_NPX + q];
+        }
+      }
+      const int y = 2 * a + py, x = 2 * b + px;
+      if (y < p.Hout && x < p.Wout)
+        st4(p.y + (((size_t)n * p.Hout + y) * p.Wout + x) * 4, f32x4{o0 + bias0, o1 + bias1, o2 + bias2, 0.f});
+    }
+  }
+}
+
+__global__ void pack_up3_kernel(const float* __restrict__ w, float* __restrict__ dst, int Cin, long total) {
+  // w: [Cin][3][5][5] (transposed-conv view); dst[it][chunk][lane][8]
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int nch = Cin / 16;
+  long t = i;
+  const int s = t % 8; t /= 8;
+  const int lane = t % 64; t /= 64;
+  const int ch = t % nch; t /= nch;
+  const int it = (int)t;
+  const int row = it * 32 + (lane & 31);
+  const int c = ch * 16 + (lane >> 5) * 8 + s;
+  float v = 0.f;
+  if (row < T3_ROWS) {
+    const int co = row / 25, tap = row % 25;
+    v = w[((size_t)c * 3 + co) * 25 + tap];
+  }
+  dst[i] = v;
+}
+
+// --------------------------------------------------------------------------
 // Weight / GDN-parameter packing
 // --------------------------------------------------------------------------
 // dst fragment (cb, outer, inner, it, lane, s) with
@@ -536,6 +656,29 @@ int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long 
   const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC);
   hipLaunchKernelGGL(pack_conv_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc, IT, CC,
                      order, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t ica_pack_up3_size(int Cin) { return (size_t)3 * (Cin / 16) * 64 * 8; }
+
+// w: transposed-conv weight view [Cin][3][5][5] contiguous (ConvTranspose2d(Cin,3) weight,
+// or Conv2d(3,Cin) weight [Cin_out=Cin][3][5][5] used for its input-gradient).
+int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t st) {
+  if (Cin % 16 != 0) return -2;
+  const long total = (long)ica_pack_up3_size(Cin);
+  hipLaunchKernelGGL(pack_up3_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, Cin, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                 hipStream_t st) {
+  if (Cin % 16 != 0) return -2;
+  ConvParams p{x, y, wp, bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, Cin, Hin, Win, 3,
+               2 * Hin, 2 * Win};
+  const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
+  hipLaunchKernelGGL(conv_up3_kernel, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }

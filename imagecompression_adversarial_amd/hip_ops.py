@@ -89,6 +89,16 @@ def conv_cc(Cin: int) -> int:
     return 4 if Cin <= 4 else 16
 
 
+def pack_up3(w_view: torch.Tensor) -> torch.Tensor:
+    """Fragments for conv_up3 from a [Cin][3][5][5] transposed-conv weight view."""
+    w = w_view.detach().contiguous()
+    _dev_check(w, "weight")
+    Cin = w.shape[0]
+    dst = torch.empty(int(lib().ica_pack_up3_size(Cin)), device=w.device)
+    call("ica_pack_up3", ptr(w), ptr(dst), Cin, stream())
+    return dst
+
+
 class PackedConv:
     """Packed fragments for one conv layer, for both its forward and its dgrad.
 
@@ -109,11 +119,17 @@ class PackedConv:
             # dgrad (conv_up): o = ci, c = co   (only k5 s2 layers have a dgrad path)
             self.bwd = None
             if self.KS == 5 and stride == 2 and self.Cout % 16 == 0:
-                self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16)
+                if self.Cin == 3:   # input-gradient of the first conv: Z-gather kernel
+                    self.bwd = pack_up3(weight)
+                else:
+                    self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16)
         elif kind == "deconv":
             self.Cin, self.Cout = weight.shape[0], weight.shape[1]
             # forward (conv_up): o = co, c = ci
-            self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16)
+            if self.Cout == 3 and self.KS == 5:
+                self.fwd = pack_up3(weight)
+            else:
+                self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16)
             # dgrad (conv_down, stride 2): o = ci, c = co
             self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,
                                  conv_cc(self.Cout))
@@ -168,6 +184,13 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     N, _, H, W, _ = x4.shape
     Ho, Wo = 2 * H, 2 * W
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
+    if Cout == 3:
+        if epi != EPI_BIAS:
+            raise RuntimeError("conv_up to 3 channels supports the bias epilogue only")
+        ev = _ev_begin(tag)
+        call("ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, stream())
+        _ev_end(ev)
+        return y, None, None
     sx = ss = None
     if save and epi in (EPI_GDN, EPI_IGDN):
         sx = empty_nc4(N, Cout, Ho, Wo, x4.device)

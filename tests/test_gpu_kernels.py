@@ -97,6 +97,20 @@ def test_dgrad_paths(K, cin, cout, hw):
     assert rel_err(K.from_nc4(gx4, cin).cpu(), xt.grad) < 2e-5
 
 
+@pytest.mark.parametrize("hw", [(32, 48), (16, 24), (18, 70)])
+def test_first_conv_dgrad_zgather(K, hw):
+    """Input-gradient of conv 3->128 (k5 s2) through the Z-gather conv_up3 kernel."""
+    H, W = hw
+    w = rnd((128, 3, 5, 5), 17) * 0.1
+    x = rnd((2, 3, 2 * H, 2 * W), 18).requires_grad_(True)
+    y = F.conv2d(x, w, None, stride=2, padding=2)
+    g = rnd(tuple(y.shape), 19)
+    y.backward(g)
+    p = K.PackedConv(w.to(dev()), None, "conv", 2)
+    gx4, _, _ = K.conv_up(K.to_nc4(g.to(dev())), 128, p.bwd, None, 3)
+    assert rel_err(K.from_nc4(gx4, 3).cpu(), x.grad) < 2e-5
+
+
 @pytest.mark.parametrize("inverse", [False, True])
 def test_gdn_epilogues(K, inverse):
     """conv_down / conv_up + fused (I)GDN forward and backward vs oracle autograd."""
