@@ -82,17 +82,13 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       }
     }
   } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
-    // requires IT*32 == Cout, co_base == 0
-    f32x16 nacc[IT];
+    // requires IT*32 == Cout, co_base == 0.  acc := x = conv + bias (kept intact
+    // until every normaliser tile is done); one 32-channel tile of
+    // n = beta' + gamma' x^2 at a time (16 accumulator registers live).
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < IT; ++it)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int c = it * 32 + acc_row(r, h);
-        acc[it][r] += p.bias ? p.bias[c] : 0.f;
-        nacc[it][r] = p.beta[c];
-      }
-    }
+      for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
     if (p.save_x && valid) {
 #pragma unroll
       for (int it = 0; it < IT; ++it)
@@ -101,11 +97,13 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           st4(p.save_x + off(it * 8 + 2 * g + h),
               f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
     }
-    // n[c][px] = beta'[c] + sum_co gamma'[c][co] x[co][px]^2  (MFMA over accumulator rows)
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int ct = 0; ct < IT; ++ct) {
+      f32x16 nacc;
 #pragma unroll
-      for (int ct = 0; ct < IT; ++ct) {
+      for (int r = 0; r < 16; ++r) nacc[r] = p.beta[ct * 32 + acc_row(r, h)];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
         const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
         const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
         const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
@@ -113,35 +111,31 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float xv = acc[it][r];
-          nacc[ct] = mfma32(ga[r], xv * xv, nacc[ct]);
+          nacc = mfma32(ga[r], xv * xv, nacc);
         }
       }
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float nv = nacc[it][r];
-        const float s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
-        nacc[it][r] = s;
-        acc[it][r] = acc[it][r] * s;
-      }
-    }
-    if (valid) {
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
+      if (valid) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const size_t o = off(it * 8 + 2 * g + h);
-          st4(p.y + o, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
-          if (p.save_s)
-            st4(p.save_s + o, f32x4{nacc[it][4 * g], nacc[it][4 * g + 1], nacc[it][4 * g + 2], nacc[it][4 * g + 3]});
+          f32x4 yv, sv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float nv = nacc[4 * g + e];
+            const float s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
+            sv[e] = s;
+            yv[e] = acc[ct][4 * g + e] * s;
+          }
+          const size_t o = off(ct * 8 + 2 * g + h);
+          st4(p.y + o, yv);
+          if (p.save_s) st4(p.save_s + o, sv);
         }
+      }
     }
   } else {  // EPI_GDN_BWD / EPI_IGDN_BWD, requires IT*32 == Cout
-    // t = (g * x) * dS/dn ; GDN: dS/dn = -0.5 s^3 ; IGDN: dS/dn = 0.5 / s.
-    // acc becomes g*s (first term of dx); x is re-read (L2-hot) for 2*x*u.
-    f32x16 tt[IT], uacc[IT];
+    // acc = g = dL/dy.  t = (g x) dS/dn (GDN: -0.5 s^3, IGDN: 0.5/s) for all
+    // channel tiles, then per output tile jt: u = gamma'^T t (16 live
+    // accumulators) and dx = g s + 2 x u with x, s re-read (L2-hot).
+    f32x16 tt[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -154,42 +148,57 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e;
-          const float gx = acc[it][r] * xv[e];
+          const float gx = acc[it][4 * g + e] * xv[e];
           const float s = sv[e];
-          tt[it][r] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
-          acc[it][r] = acc[it][r] * s;
-          uacc[it][r] = 0.f;
+          tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
         }
       }
-    // u[j][px] = sum_c gamma'[c][j] t[c][px]
 #pragma unroll
-    for (int ct = 0; ct < IT; ++ct) {
+    for (int jt = 0; jt < IT; ++jt) {
+      f32x16 uacc = f32x16{0};
 #pragma unroll
-      for (int jt = 0; jt < IT; ++jt) {
+      for (int ct = 0; ct < IT; ++ct) {
         const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
         const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
         const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
                               g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) uacc[jt] = mfma32(ga[r], tt[ct][r], uacc[jt]);
+        for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
       }
-    }
-    if (valid) {
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
+      if (valid) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const size_t o = off(it * 8 + 2 * g + h);
-          const f32x4 xv = ld4(p.in_x + o);
+          const size_t o = off(jt * 8 + 2 * g + h);
+          const f32x4 xv = ld4(p.in_x + o), sv = ld4(p.in_s + o);
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
-            v[e] = acc[it][r] + 2.0f * xv[e] * uacc[it][r];
+            v[e] = acc[jt][r] * sv[e] + 2.0f * xv[e] * uacc[r];
           }
           st4(p.y + o, v);
         }
+      }
+    }
+  }
+}
+
+// Load one (chunk, tap) weight fragment set: IT tiles x KH floats per lane.
+template <int IT, int KH>
+ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    if constexpr (KH == 8) {
+      const f32x4 w0 = ld4(w + it * 64 * KH), w1 = ld4(w + it * 64 * KH + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[it][e] = w0[e];
+        a[it][4 + e] = w1[e];
+      }
+    } else {
+      const f32x2 w0 = *reinterpret_cast<const f32x2*>(w + it * 64 * KH);
+      a[it][0] = w0[0];
+      a[it][1] = w0[1];
     }
   }
 }
@@ -200,7 +209,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 // c = chunk*CC + (lane>>5)*KH + s.
 // --------------------------------------------------------------------------
 template <int KS, int S, int IT, int CC, int TW, int EPI>
-__global__ __launch_bounds__(256) void conv_down_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   constexpr int TH = 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
   constexpr int NQ = CC / 4, KH = CC / 2, PLANE = PR * PC, PAD = KS / 2;
@@ -225,62 +234,65 @@ __global__ __launch_bounds__(256) void conv_down_kernel(ConvParams p) {
 #pragma unroll
   for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
 
-  const float* wcb = p.wp + (size_t)cb * nch * KS * KS * WSTEP + (size_t)lane * KH;
+  // Weight fragments stream linearly through (chunk, tap); they are prefetched
+  // one tap ahead into the other of two register sets (ping-pong, no copies)
+  // so each tap's MFMAs cover the next tap's global (L2-resident) load latency.
+  const float* wptr = p.wp + (size_t)cb * nch * KS * KS * WSTEP + (size_t)lane * KH;
+  constexpr int KK = KS * KS;
+  const int total = nch * KK;
   const int lbase = (S * oyl) * PC + S * oxl;
-
-  for (int ch = 0; ch < nch; ++ch) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < NQ * PLANE; e += 256) {
-      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
-      const int c4 = ch * NQ + q, iy = iy0 + pr, ix = ix0 + pc;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win)
-        v = ld4(p.x + ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4);
-      patch[e] = v;
-    }
-    __syncthreads();
-    const float* wch = wcb + (size_t)ch * KS * KS * WSTEP;
+  auto step = [&](float (&cur)[IT][KH], float (&nxt)[IT][KH], int g) {
+    const int ch = g / KK, tap = g - ch * KK;
+    if (tap == 0) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < NQ * PLANE; e += 256) {
+        const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+        const int c4 = ch * NQ + q, iy = iy0 + pr, ix = ix0 + pc;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
+          v = ld4(p.x + ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4);
+          if constexpr (CC == 4) {
 #pragma unroll
-    for (int tap = 0; tap < KS * KS; ++tap) {
-      const int ky = tap / KS, kx = tap % KS;
-      float b[KH];
-      if constexpr (CC == 16) {
-        const f32x4 v0 = patch[(2 * h) * PLANE + lbase + ky * PC + kx];
-        const f32x4 v1 = patch[(2 * h + 1) * PLANE + lbase + ky * PC + kx];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          b[e] = v0[e];
-          b[4 + e] = v1[e];
-        }
-      } else {  // CC == 4
-        const float* pf = reinterpret_cast<const float*>(&patch[lbase + ky * PC + kx]) + 2 * h;
-        const f32x2 v = *reinterpret_cast<const f32x2*>(pf);
-        b[0] = v[0];
-        b[1] = v[1];
-      }
-      const float* wt = wch + (size_t)tap * WSTEP;
-      float a[IT][KH];
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        if constexpr (KH == 8) {
-          const f32x4 w0 = ld4(wt + it * 64 * KH), w1 = ld4(wt + it * 64 * KH + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            a[it][e] = w0[e];
-            a[it][4 + e] = w1[e];
+            for (int e2 = 0; e2 < 4; ++e2)
+              if (c4 * 4 + e2 >= p.Cin) v[e2] = 0.f;
           }
-        } else {
-          const f32x2 w0 = *reinterpret_cast<const f32x2*>(wt + it * 64 * KH);
-          a[it][0] = w0[0];
-          a[it][1] = w0[1];
         }
+        patch[e] = v;
       }
-#pragma unroll
-      for (int s = 0; s < KH; ++s)
-#pragma unroll
-        for (int it = 0; it < IT; ++it) acc[it] = mfma32(a[it][s], b[s], acc[it]);
+      __syncthreads();
     }
+    load_frag<IT, KH>(nxt, wptr + (size_t)min(g + 1, total - 1) * WSTEP);  // unconditional: no phi copies
+    const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+    const int lo = lbase + ky * PC + kx;
+    float b[KH];
+    if constexpr (CC == 16) {
+      const f32x4 v0 = patch[(2 * h) * PLANE + lo];
+      const f32x4 v1 = patch[(2 * h + 1) * PLANE + lo];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        b[e] = v0[e];
+        b[4 + e] = v1[e];
+      }
+    } else {  // CC == 4
+      const float* pf = reinterpret_cast<const float*>(&patch[lo]) + 2 * h;
+      const f32x2 v = *reinterpret_cast<const f32x2*>(pf);
+      b[0] = v[0];
+      b[1] = v[1];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < KH; ++s2)
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+  };
+  float fa[IT][KH], fb[IT][KH];
+  load_frag<IT, KH>(fa, wptr);
+  int g = 0;
+#pragma unroll 1
+  for (; g + 1 < total; g += 2) {
+    step(fa, fb, g);
+    step(fb, fa, g + 1);
   }
+  if (g < total) step(fa, fb, g);
   const int oy = oy0 + oyl, ox = ox0 + oxl;
   conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
@@ -298,44 +310,47 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int a_rel = jt * 2 + (j >> 4), b_rel = j & 15;
   constexpr int WSTEP = IT * 64 * 8;
+  constexpr int NY = (5 - PY + 1) / 2, NX = (5 - PX + 1) / 2;  // taps per axis (3 or 2)
   const float* wl = p.wp + (size_t)cb * 25 * nch * WSTEP + (size_t)lane * 8;
   f32x16 acc[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+  // (tap, chunk) sequence flattened; weight fragments prefetched one step ahead
+  // into the other of two register sets (ping-pong).
+  const int total = NY * NX * nch;
+  auto wptr = [&](int u) {
+    const int ti = u / nch, ch = u - ti * nch;
+    const int ky = PY + 2 * (ti / NX), kx = PX + 2 * (ti % NX);
+    return wl + ((size_t)(ky * 5 + kx) * nch + ch) * WSTEP;
+  };
+  auto step = [&](float (&cur)[IT][8], float (&nxt)[IT][8], int u) {
+    load_frag<IT, 8>(nxt, wptr(min(u + 1, total - 1)));  // unconditional: no phi copies
+    const int ti = u / nch, ch = u - ti * nch;
+    const int ky = PY + 2 * (ti / NX), kx = PX + 2 * (ti % NX);
+    const int pr = a_rel + 1 + (PY + 2 - ky) / 2, pc = b_rel + 1 + (PX + 2 - kx) / 2;
+    const f32x4* pp = patch + (4 * ch + 2 * h) * UP_PLANE + pr * UP_PC + pc;
+    const f32x4 v0 = pp[0], v1 = pp[UP_PLANE];
+    const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 #pragma unroll
-  for (int ky = PY; ky < 5; ky += 2) {
+    for (int s2 = 0; s2 < 8; ++s2)
 #pragma unroll
-    for (int kx = PX; kx < 5; kx += 2) {
-      const int pr = a_rel + 1 + (PY + 2 - ky) / 2, pc = b_rel + 1 + (PX + 2 - kx) / 2;
-      const f32x4* pp = patch + (2 * h) * UP_PLANE + pr * UP_PC + pc;
-      const float* wt = wl + (size_t)(ky * 5 + kx) * nch * WSTEP;
-
-      for (int ch = 0; ch < nch; ++ch) {
-        const f32x4 v0 = pp[(4 * ch) * UP_PLANE], v1 = pp[(4 * ch + 1) * UP_PLANE];
-        const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        float a[IT][8];
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          const f32x4 w0 = ld4(wt + (size_t)ch * WSTEP + it * 512), w1 = ld4(wt + (size_t)ch * WSTEP + it * 512 + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            a[it][e] = w0[e];
-            a[it][4 + e] = w1[e];
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < 8; ++s)
-#pragma unroll
-          for (int it = 0; it < IT; ++it) acc[it] = mfma32(a[it][s], b[s], acc[it]);
-      }
-    }
+      for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+  };
+  float fa[IT][8], fb[IT][8];
+  load_frag<IT, 8>(fa, wptr(0));
+  int u = 0;
+#pragma unroll 1
+  for (; u + 1 < total; u += 2) {
+    step(fa, fb, u);
+    step(fb, fa, u + 1);
   }
+  if (u < total) step(fa, fb, u);
   const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
   conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
 template <int IT, int EPI>
-__global__ __launch_bounds__(256) void conv_up_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   extern __shared__ f32x4 patch[];  // [Cin4][UP_PR][UP_PC]
   const int Hh = p.Hin, Wh = p.Win;
   const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UP_TH - 1) / UP_TH;

@@ -1,0 +1,118 @@
+/*
+ * ica_hip.h — C ABI of libica_hip.so, the MI355X (gfx950) drop-in for the
+ * adversarial-attack hot path of tongxyh/ImageCompression_Adversarial.
+ *
+ * Conventions
+ *   - All tensor arguments are device pointers (fp32) allocated and owned by
+ *     the caller (PyTorch's caching allocator); the library never allocates
+ *     or frees caller memory and never synchronises the stream.
+ *   - Activation tensors on the hot path use the nChw4c layout
+ *     [N][ceil(C/4)][H][W][4]; padded channels are zero.  Image-domain tensors
+ *     (noise, im_s, output_s, m, v) are plain NCHW [B][3][H][W].
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream).
+ *   - Every function returns 0 on success, a hipError_t from the launch, or a
+ *     negative code for an unsupported shape/variant (-2 channel multiple,
+ *     -3 channel tile, -4 epilogue/shape mismatch, -5 epilogue id, -6 kernel
+ *     geometry).  The Python layer turns non-zero into RuntimeError.
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   conv / deconv layers + autograd dgrad .......... anchors/utils.py:112-130 (via CompressAI g_a/g_s, h_a/h_s)
+ *   GDN / IGDN (fwd + bwd) .......................... utils/ops.py:58-97  (== compressai.layers.GDN)
+ *   Low_bound / Up_bound (clamp + pass-through) ..... utils/ops.py:28-56
+ *   attack step (box, clamp, L2 loss, branch, Adam)  attack_rd.py:496-559, attack_our :332-379
+ *   I-FGSM / MI-FGSM update + projection ........... attack_ifgsm.py:348-362, 405-419
+ *   EntropyBottleneck / GaussianConditional lik. ... anchors/model.py:86-108, anchors/balle.py:31-55 (CompressAI)
+ *   bpp ............................................. attack_rd.py:419, self_ensemble.py:222
+ *   MS-SSIM (pytorch_msssim / utils.torch_msssim) .. attack_rd.py:336,362; utils/torch_msssim.py:26-71
+ */
+#ifndef ICA_HIP_H
+#define ICA_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+/* ---- conv engine (ica_conv.hip) ------------------------------------------- */
+/* epilogue ids */
+enum { ICA_EPI_BIAS = 0, ICA_EPI_RELU = 1, ICA_EPI_GDN = 2, ICA_EPI_IGDN = 3, ICA_EPI_GDN_BWD = 4, ICA_EPI_IGDN_BWD = 5 };
+
+/* 32-channel MFMA row tiles per wave the launchers use for `cout` output channels. */
+int ica_conv_it(int cout);
+/* floats needed for the packed fragments of a weight viewed as W[O][C][KS][KS], chunk CC (4|16). */
+size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC);
+/* Pack W (element (o,c,ky,kx) at w[o*so + c*sc + ky*KS + kx]); order 0 = conv_down, 1 = conv_up. */
+int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long so, long sc, int CC, int order,
+                         hipStream_t stream);
+/* GDN reparametrisation + fragment packing: gamma' = max(gamma,2^-18)^2 - 2^-36 (transpose 0: gamma', 1: gamma'^T),
+ * beta_eff = max(beta, beta_bound)^2 - 2^-36.  gp holds (C/32)^2 * 1024 floats. */
+int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_eff, int C, int transpose,
+                 float beta_bound, hipStream_t stream);
+/* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
+ * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
+ * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,
+ * gp = gamma'^T fragments, in_x/in_s = the saved x/s of that GDN; y receives dL/dx. */
+int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                  int Cout, int Hout, int Wout, int KS, int S, int epi, const float* gp, const float* beta,
+                  float* save_x, float* save_s, const float* in_x, const float* in_s, hipStream_t stream);
+/* y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+ epilogue); Cin % 16 == 0. */
+int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                int Cout, int Hout, int Wout, int epi, const float* gp, const float* beta, float* save_x,
+                float* save_s, const float* in_x, const float* in_s, hipStream_t stream);
+/* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
+size_t ica_pack_up3_size(int Cin);
+int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t stream);
+int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                 hipStream_t stream);
+
+/* ---- elementwise / attack step / entropy (ica_elem.hip) -------------------- */
+int ica_elem_blocks_per_image(void);
+int ica_nchw_to_nc4(const float* src, float* dst, int N, int C, int H, int W, hipStream_t stream);
+int ica_nc4_to_nchw(const float* src, float* dst, int N, int C, int H, int W, hipStream_t stream);
+/* out[b] = scale * sum_k part[b*nblk + k] (deterministic order). */
+int ica_reduce_rows(const float* part, float* out, int B, int nblk, float scale, hipStream_t stream);
+/* im_in4 = Up(Low(im_s + Up(Low(noise,-eps),eps), 0), 1) (nChw4c) ; part = per-image partial sum (im_s-im_in)^2. */
+int ica_attack_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
+                        float eps, hipStream_t stream);
+/* mode 0: dL/dx_hat of 1 - mean((os - bound01(x_hat))^2) (clamp optional); mode 1: of mean((os - x_hat)^2). */
+int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float* part, int B, int H, int W,
+                    float invN, int clamp, int mode, hipStream_t stream);
+/* Per-image branch (loss_i[b] > thr), bounds backward, torch-Adam step on noise/m/v (in place). */
+int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
+                    float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
+                    float bc2s, float neg_step, int* branch, hipStream_t stream);
+int ica_ifgsm_step(float* x, const float* im_s, const float* grad4, float* gacc, const float* l1, int B, int H, int W,
+                   float alpha, float eps, int momentum, hipStream_t stream);
+int ica_l1_partial(const float* g4, float* part, int B, int H, int W, hipStream_t stream);
+int ica_gc_likelihood(const float* y, const float* scales, const float* means, const float* qnoise, float* y_hat,
+                      float* lik, float* part, int B, int C, int H, int W, int training, hipStream_t stream);
+int ica_eb_likelihood(const float* z, const float* prm, const float* med, const float* qnoise, float* z_hat,
+                      float* lik, float* part, int B, int C, int H, int W, int training, hipStream_t stream);
+/* params: host array of 15 device pointers (_matrix0..4, _bias0..4, _factor0..3, quantiles). */
+int ica_pack_eb(const float* const* params, float* prm, float* med, int C, hipStream_t stream);
+int ica_abs(const float* x, float* y, long n, hipStream_t stream);
+int ica_clamp01(const float* x, float* y, long n, hipStream_t stream);
+int ica_sqdiff_partial(const float* a, const float* b, float* part, int B, long len, int clamp_a, hipStream_t stream);
+int ica_nc4_bound_to_nchw(const float* x4, float* out, int B, int H, int W, int clamp, hipStream_t stream);
+int ica_bound_bwd_nc4(const float* x4, const float* g, float* g4, int B, int H, int W, int clamp, hipStream_t stream);
+
+/* ---- MS-SSIM (ica_msssim.hip) ---------------------------------------------- */
+/* mode 0 = pytorch_msssim (valid, per-channel, relu), mode 1 = utils/torch_msssim (same-pad, global). */
+int ica_msssim_blocks(int H, int W, int ws, int mode);
+int ica_msssim_level(const float* X, const float* Y, int P, int H, int W, const float* win_host, int ws, int mode,
+                     float C1, float C2, float* part, float* out, float* maps, const float* wgt, hipStream_t stream);
+int ica_msssim_level_bwd(const float* X, const float* Y, const float* maps, int P, int H, int W, const float* win_host,
+                         int ws, int mode, float* gX, float* gY, hipStream_t stream);
+int ica_msssim_combine(const float* lvl, int P, int G, int mode, const float* dval, float* val, float* wgt,
+                       const float* nout_host, hipStream_t stream);
+int ica_avgpool2(const float* X, float* Y, int P, int H, int W, int ph, int pw, hipStream_t stream);
+int ica_avgpool2_bwd(const float* gO, float* gX, int P, int H, int W, int ph, int pw, hipStream_t stream);
+int ica_scale(float* x, long n, float s, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICA_HIP_H */
