@@ -1,0 +1,434 @@
+"""CompressAI-compatible codec modules running on the HIP kernels.
+
+Replaces the un-vendored third-party surface the reference drives
+(anchors/model.py:3-5, anchors/balle.py:7-8): ``bmshj2018_factorized`` /
+``bmshj2018_hyperprior`` models with ``g_a``, ``g_s``, ``h_a``, ``h_s``,
+``entropy_bottleneck``, ``gaussian_conditional``, ``forward(x) ->
+{"x_hat", "likelihoods"}``, ``aux_loss()`` and CompressAI state-dict keys
+(``g_a.0.weight``, ``g_a.1.beta``, ``g_a.1.gamma``, ``g_a.1.beta_reparam.pedestal``,
+``entropy_bottleneck._matrix0``, ``entropy_bottleneck.quantiles``, ...).
+
+``g_a`` / ``g_s`` are nn.Sequential containers (so parameters and indexing
+look like CompressAI's) whose forward runs the fused HIP chain as one
+autograd Function: forward saves the GDN activations, backward runs the fused
+dgrad chain.  Weight gradients are not produced on this path (the attack
+freezes the codec); see ``requires_grad`` note in DESIGN.md.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import engine as E
+from . import hip_ops as K
+
+# --------------------------------------------------------------------------- #
+# Parametrizers (compressai.ops.parametrizers / bound_ops; utils/ops.py:58-97)
+# --------------------------------------------------------------------------- #
+
+
+class LowerBound(nn.Module):
+    def __init__(self, bound: float):
+        super().__init__()
+        self.register_buffer("bound", torch.Tensor([float(bound)]))
+
+    def forward(self, x):
+        return torch.max(x, self.bound)
+
+
+class NonNegativeParametrizer(nn.Module):
+    def __init__(self, minimum: float = 0.0, reparam_offset: float = 2 ** -18):
+        super().__init__()
+        self.minimum = float(minimum)
+        self.reparam_offset = float(reparam_offset)
+        pedestal = self.reparam_offset ** 2
+        self.register_buffer("pedestal", torch.Tensor([pedestal]))
+        bound = (self.minimum + self.reparam_offset ** 2) ** 0.5
+        self.lower_bound = LowerBound(bound)
+
+    def init(self, x):
+        return torch.sqrt(torch.max(x + self.pedestal, self.pedestal))
+
+    def forward(self, x):
+        return self.lower_bound(x) ** 2 - self.pedestal
+
+
+class GDN(nn.Module):
+    """GDN / IGDN parameters (compressai.layers.GDN == utils/ops.py:58-97).  Inside g_a/g_s the
+    normalisation runs fused in the producing conv's epilogue; stand-alone use is not supported."""
+
+    def __init__(self, in_channels: int, inverse: bool = False, beta_min: float = 1e-6, gamma_init: float = 0.1):
+        super().__init__()
+        self.inverse = bool(inverse)
+        self.beta_reparam = NonNegativeParametrizer(minimum=float(beta_min))
+        self.beta = nn.Parameter(self.beta_reparam.init(torch.ones(in_channels)))
+        self.gamma_reparam = NonNegativeParametrizer()
+        self.gamma = nn.Parameter(self.gamma_reparam.init(float(gamma_init) * torch.eye(in_channels)))
+
+    def forward(self, x):
+        raise RuntimeError("GDN runs fused inside g_a/g_s on this backend; call the transform, not the layer")
+
+
+def conv(in_channels, out_channels, kernel_size=5, stride=2):
+    """anchors/utils.py:112-119."""
+    return nn.Conv2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride, padding=kernel_size // 2)
+
+
+def deconv(in_channels, out_channels, kernel_size=5, stride=2):
+    """anchors/utils.py:122-130."""
+    return nn.ConvTranspose2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride,
+                              output_padding=stride - 1, padding=kernel_size // 2)
+
+
+# --------------------------------------------------------------------------- #
+# Fused transforms
+# --------------------------------------------------------------------------- #
+
+
+def _state(module: nn.Module) -> dict:
+    return {k: v for k, v in module.state_dict(keep_vars=True).items()}
+
+
+def _key(module: nn.Module):
+    return tuple((p.data_ptr(), p._version) for p in module.parameters())
+
+
+class _TransformFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, module, *params):
+        ex = module._executor()
+        need = ctx.needs_input_grad[0]
+        out4, saved = ex.forward(K.to_nc4(x.detach().contiguous()), save=need)
+        ctx.ex, ctx.saved, ctx.cin = ex, saved, x.shape[1]
+        return K.from_nc4(out4, module.out_channels)
+
+    @staticmethod
+    def backward(ctx, gy):
+        gx4 = ctx.ex.backward(K.to_nc4(gy.contiguous()), ctx.saved)
+        ctx.saved = None
+        return (K.from_nc4(gx4, ctx.cin), None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+class _FusedSequential(nn.Sequential):
+    _exec_cls = None
+
+    def __init__(self, *layers):
+        super().__init__(*layers)
+        self._ex = None
+        self._ex_key = None
+        self._warned = False
+
+    def _executor(self):
+        k = _key(self)
+        if self._ex is None or self._ex_key != k:
+            self._ex = self._make_executor(_state(self))
+            self._ex_key = k
+        return self._ex
+
+    def forward(self, x):
+        if not torch.is_grad_enabled():
+            out4, _ = self._executor().forward(K.to_nc4(x.detach().contiguous()), save=False)
+            return K.from_nc4(out4, self.out_channels)
+        if not self._warned and any(p.requires_grad for p in self.parameters()):
+            self._warned = True
+            warnings.warn("codec weight gradients are not computed on the HIP attack path (input gradients "
+                          "only); freeze the codec with requires_grad_(False) to silence this", stacklevel=2)
+        return _TransformFn.apply(x, self, *self.parameters())
+
+
+class AnalysisTransform(_FusedSequential):
+    """g_a: conv(3,N)-GDN-conv(N,N)-GDN-conv(N,N)-GDN-conv(N,M) (CompressAI bmshj2018)."""
+
+    def __init__(self, N, M):
+        super().__init__(conv(3, N), GDN(N), conv(N, N), GDN(N), conv(N, N), GDN(N), conv(N, M))
+        self.out_channels = M
+
+    def _make_executor(self, sd):
+        return E.Analysis(sd, prefix="")
+
+
+class SynthesisTransform(_FusedSequential):
+    """g_s: deconv(M,N)-IGDN-deconv(N,N)-IGDN-deconv(N,N)-IGDN-deconv(N,3)."""
+
+    def __init__(self, N, M):
+        super().__init__(deconv(M, N), GDN(N, inverse=True), deconv(N, N), GDN(N, inverse=True),
+                         deconv(N, N), GDN(N, inverse=True), deconv(N, 3))
+        self.out_channels = 3
+
+    def _make_executor(self, sd):
+        return E.Synthesis(sd, prefix="")
+
+
+class _ForwardOnly(nn.Sequential):
+    def __init__(self, *layers):
+        super().__init__(*layers)
+        self._ex = None
+        self._ex_key = None
+
+    def _executor(self):
+        k = _key(self)
+        if self._ex is None or self._ex_key != k:
+            self._ex = self._make_executor(_state(self))
+            self._ex_key = k
+        return self._ex
+
+    def forward(self, x):
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            if x.requires_grad:
+                raise NotImplementedError("hyperprior transforms are forward-only on the HIP path")
+        out4 = self._run(self._executor(), K.to_nc4(x.detach().contiguous()))
+        return K.from_nc4(out4, self.out_channels)
+
+
+class HyperAnalysisTransform(_ForwardOnly):
+    """h_a = conv(M,N,3,1)-ReLU-conv(N,N)-ReLU-conv(N,N)."""
+
+    def __init__(self, N, M):
+        super().__init__(conv(M, N, stride=1, kernel_size=3), nn.ReLU(inplace=True), conv(N, N),
+                         nn.ReLU(inplace=True), conv(N, N))
+        self.out_channels = N
+
+    def _make_executor(self, sd):
+        return E.HyperAnalysis(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4, take_abs=False)
+
+
+class HyperSynthesisTransform(_ForwardOnly):
+    """h_s = deconv(N,N)-ReLU-deconv(N,N)-ReLU-conv(N,M,3,1)-ReLU."""
+
+    def __init__(self, N, M):
+        super().__init__(deconv(N, N), nn.ReLU(inplace=True), deconv(N, N), nn.ReLU(inplace=True),
+                         conv(N, M, stride=1, kernel_size=3), nn.ReLU(inplace=True))
+        self.out_channels = M
+
+    def _make_executor(self, sd):
+        return E.HyperSynthesis(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4)
+
+
+# --------------------------------------------------------------------------- #
+# Entropy models (compressai.entropy_models)
+# --------------------------------------------------------------------------- #
+
+
+class EntropyModel(nn.Module):
+    def __init__(self, likelihood_bound: float = 1e-9):
+        super().__init__()
+        self.use_likelihood_bound = likelihood_bound > 0
+        self.likelihood_lower_bound = LowerBound(likelihood_bound)
+        self.register_buffer("_offset", torch.IntTensor())
+        self.register_buffer("_quantized_cdf", torch.IntTensor())
+        self.register_buffer("_cdf_length", torch.IntTensor())
+
+    def quantize(self, inputs, mode, means=None):
+        """CompressAI EntropyModel.quantize ("noise" | "dequantize" | "symbols"); round = half-to-even."""
+        if mode not in ("noise", "dequantize", "symbols"):
+            raise ValueError(f'Invalid quantization mode: "{mode}"')
+        if mode == "noise":
+            return inputs + torch.empty_like(inputs).uniform_(-0.5, 0.5)
+        outputs = inputs.clone()
+        if means is not None:
+            outputs -= means
+        outputs = torch.round(outputs)
+        if mode == "dequantize":
+            if means is not None:
+                outputs += means
+            return outputs
+        return outputs.int()
+
+
+class EntropyBottleneck(EntropyModel):
+    def __init__(self, channels, tail_mass=1e-9, init_scale=10, filters=(3, 3, 3, 3)):
+        super().__init__()
+        self.channels = int(channels)
+        self.filters = tuple(int(f) for f in filters)
+        self.init_scale = float(init_scale)
+        self.tail_mass = float(tail_mass)
+        filters = (1,) + self.filters + (1,)
+        scale = self.init_scale ** (1 / (len(self.filters) + 1))
+        for i in range(len(self.filters) + 1):
+            init = math.log(math.expm1(1 / scale / filters[i + 1]))
+            self.register_parameter(f"_matrix{i:d}",
+                                    nn.Parameter(torch.full((channels, filters[i + 1], filters[i]), init)))
+            self.register_parameter(f"_bias{i:d}",
+                                    nn.Parameter(torch.empty(channels, filters[i + 1], 1).uniform_(-0.5, 0.5)))
+            if i < len(self.filters):
+                self.register_parameter(f"_factor{i:d}", nn.Parameter(torch.zeros(channels, filters[i + 1], 1)))
+        self.quantiles = nn.Parameter(torch.Tensor([-self.init_scale, 0, self.init_scale]).repeat(channels, 1, 1))
+        target = math.log(2 / self.tail_mass - 1)
+        self.register_buffer("target", torch.Tensor([-target, 0, target]))
+        self._packed = None
+        self._packed_key = None
+
+    def _pack(self):
+        names = K.PackedEB.NAMES
+        k = tuple((getattr(self, n).data_ptr(), getattr(self, n)._version) for n in names)
+        if self._packed is None or self._packed_key != k:
+            self._packed = K.PackedEB({n: getattr(self, n) for n in names})
+            self._packed_key = k
+        return self._packed
+
+    def _logits_cumulative(self, inputs, stop_gradient: bool):
+        logits = inputs
+        for i in range(len(self.filters) + 1):
+            matrix = getattr(self, f"_matrix{i:d}")
+            bias = getattr(self, f"_bias{i:d}")
+            if stop_gradient:
+                matrix, bias = matrix.detach(), bias.detach()
+            logits = torch.matmul(F.softplus(matrix), logits) + bias
+            if i < len(self.filters):
+                factor = getattr(self, f"_factor{i:d}")
+                if stop_gradient:
+                    factor = factor.detach()
+                logits = logits + torch.tanh(factor) * torch.tanh(logits)
+        return logits
+
+    def loss(self):
+        """Aux loss on the quantiles (parameter-only, C x 3 values; train.py:364, adv_train.py:190)."""
+        logits = self._logits_cumulative(self.quantiles, stop_gradient=True)
+        return torch.abs(logits - self.target).sum()
+
+    def _get_medians(self):
+        return self.quantiles[:, :, 1:2]
+
+    def forward(self, x, training=None):
+        if training is None:
+            training = self.training
+        C = x.shape[1]
+        noise4 = None
+        if training:
+            noise4 = K.to_nc4(torch.empty_like(x).uniform_(-0.5, 0.5))
+        zh4, lik4, _ = K.eb_likelihood(K.to_nc4(x.detach().contiguous()), C, self._pack(), training, noise4)
+        return K.from_nc4(zh4, C), K.from_nc4(lik4, C)
+
+
+class GaussianConditional(EntropyModel):
+    def __init__(self, scale_table=None, scale_bound=0.11, tail_mass=1e-9):
+        super().__init__()
+        self.tail_mass = float(tail_mass)
+        self.register_buffer("scale_table", torch.Tensor(tuple(scale_table) if scale_table else ()))
+        self.register_buffer("scale_bound", torch.Tensor([float(scale_bound)]))
+        self.lower_bound_scale = LowerBound(scale_bound)
+
+    def forward(self, inputs, scales, means=None, training=None):
+        if training is None:
+            training = self.training
+        C = inputs.shape[1]
+        noise4 = K.to_nc4(torch.empty_like(inputs).uniform_(-0.5, 0.5)) if training else None
+        m4 = K.to_nc4(means.detach().contiguous()) if means is not None else None
+        yh4, lik4, _ = K.gc_likelihood(K.to_nc4(inputs.detach().contiguous()), C,
+                                       K.to_nc4(scales.detach().contiguous()), m4, training, noise4)
+        return K.from_nc4(yh4, C), K.from_nc4(lik4, C)
+
+
+# --------------------------------------------------------------------------- #
+# Models (CompressAI bmshj2018)
+# --------------------------------------------------------------------------- #
+
+
+class CompressionModel(nn.Module):
+    def aux_loss(self):
+        return sum(m.loss() for m in self.modules() if isinstance(m, EntropyBottleneck))
+
+    def load_state_dict(self, state_dict, strict=True):
+        # CompressAI buffers with checkpoint-dependent sizes (anchors/utils.py:74-109)
+        for name, mod in self.named_modules():
+            if isinstance(mod, EntropyModel):
+                for b in ("_offset", "_quantized_cdf", "_cdf_length", "scale_table"):
+                    key = f"{name}.{b}"
+                    if key in state_dict and hasattr(mod, b):
+                        getattr(mod, b).resize_(state_dict[key].size())
+        return super().load_state_dict(state_dict, strict=strict)
+
+    def kernels(self):
+        """Whole-model HIP executor (used by the attack engine)."""
+        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        if getattr(self, "_ck", None) is None or self._ck_key != key:
+            sd = {k: v.detach() for k, v in self.state_dict().items()}
+            self._ck = E.CodecKernels(sd, self.model_kind)
+            self._ck_key = key
+        return self._ck
+
+
+class FactorizedPrior(CompressionModel):
+    model_kind = "factorized"
+
+    def __init__(self, N, M, **kwargs):
+        super().__init__()
+        self.entropy_bottleneck = EntropyBottleneck(M)
+        self.g_a = AnalysisTransform(N, M)
+        self.g_s = SynthesisTransform(N, M)
+        self.N, self.M = int(N), int(M)
+
+    def forward(self, x):
+        y = self.g_a(x)
+        y_hat, y_likelihoods = self.entropy_bottleneck(y)
+        x_hat = self.g_s(y_hat)
+        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods}}
+
+
+class ScaleHyperprior(CompressionModel):
+    model_kind = "hyper"
+
+    def __init__(self, N, M, **kwargs):
+        super().__init__()
+        self.entropy_bottleneck = EntropyBottleneck(N)
+        self.g_a = AnalysisTransform(N, M)
+        self.g_s = SynthesisTransform(N, M)
+        self.h_a = HyperAnalysisTransform(N, M)
+        self.h_s = HyperSynthesisTransform(N, M)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.N, self.M = int(N), int(M)
+
+    def forward(self, x):
+        y = self.g_a(x)
+        z = self.h_a(torch.abs(y))
+        z_hat, z_likelihoods = self.entropy_bottleneck(z)
+        scales_hat = self.h_s(z_hat)
+        y_hat, y_likelihoods = self.gaussian_conditional(y, scales_hat)
+        x_hat = self.g_s(y_hat)
+        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+
+
+# --------------------------------------------------------------------------- #
+# Zoo constructors (compressai.zoo)
+# --------------------------------------------------------------------------- #
+_CFG = {
+    "bmshj2018-factorized": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
+    "bmshj2018-hyperprior": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
+}
+
+
+def _load_pretrained(model, arch, quality, metric):
+    """Pretrained zoo weights need a download the offline box cannot do (coder.py:96-101).
+    A local CompressAI-format file is used when present: $TORCH_HOME/checkpoints/<arch>-<quality>-<metric>*.pth*"""
+    import glob
+    import os
+    home = os.environ.get("TORCH_HOME", "./ckpts/torch/")
+    pats = glob.glob(os.path.join(home, "checkpoints", f"{arch}-{quality}*"))
+    if not pats:
+        raise RuntimeError(f"pretrained {arch} q{quality} ({metric}) needs a network download; place the "
+                           f"CompressAI checkpoint under {home}/checkpoints or pass -ckpt")
+    sd = torch.load(pats[0], map_location="cpu", weights_only=True)
+    model.load_state_dict(sd.get("state_dict", sd))
+    return model
+
+
+def bmshj2018_factorized(quality, metric="mse", pretrained=False, progress=True, **kwargs):
+    N, M = _CFG["bmshj2018-factorized"][quality]
+    m = FactorizedPrior(N, M)
+    return _load_pretrained(m, "bmshj2018-factorized", quality, metric) if pretrained else m
+
+
+def bmshj2018_hyperprior(quality, metric="mse", pretrained=False, progress=True, **kwargs):
+    N, M = _CFG["bmshj2018-hyperprior"][quality]
+    m = ScaleHyperprior(N, M)
+    return _load_pretrained(m, "bmshj2018-hyperprior", quality, metric) if pretrained else m

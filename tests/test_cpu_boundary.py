@@ -1,0 +1,92 @@
+"""CPU-side checks of the C-ABI boundary and the host mirror of the reference interface
+(no GPU compute): the library loads and exports every symbol include/ica_hip.h declares;
+the CLI keeps the reference flags and defaults (coder.py:166-220); image I/O rounding."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "ica_hip.h")).read()
+    return sorted(set(re.findall(r"^(?:int|size_t)\s+(ica_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_header_symbols():
+    from imagecompression_adversarial_amd import _lib
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    # every binding the Python layer declares is in the header too
+    assert set(_lib.exported_symbols()) <= set(syms)
+
+
+def test_no_oracle_import_in_product():
+    pkg = os.path.join(REPO, "imagecompression_adversarial_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(root, f)).read()
+                assert "from oracle" not in src and "import oracle" not in src, f
+
+
+def test_cli_flags_and_defaults():
+    from imagecompression_adversarial_amd import coder
+    a = coder.config().parse_args([])
+    assert (a.model, a.metric, a.quality, a.steps, a.noise, a.epsilon, a.lr_attack, a.att_metric, a.random,
+            a.clamp, a.device) == ("hyper", "ms-ssim", 3, 1001, 1e-4, 16.0, 0.01, "L2", 1, True, "cuda:0")
+    a = coder.config().parse_args(["-m", "hyper", "-metric", "mse", "-q", "1", "-s", "x.png", "--no-clamp"])
+    assert (a.model, a.metric, a.quality, a.source, a.clamp) == ("hyper", "mse", 1, "x.png", False)
+
+
+def test_read_write_image_roundtrip(tmp_path):
+    from PIL import Image
+    from imagecompression_adversarial_amd import coder
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, size=(50, 70, 3), dtype=np.uint8)
+    p = tmp_path / "a.png"
+    Image.fromarray(img).save(p)
+    x, H, W = coder.read_image(str(p))
+    assert x.shape == (1, 3, 64, 128) and (H, W) == (50, 70)
+    assert float(x[:, :, 50:, :].abs().max()) == 0.0 and float(x[:, :, :, 70:].abs().max()) == 0.0
+    q = tmp_path / "b.png"
+    coder.write_image(x, str(q), H, W)
+    assert np.array_equal(np.array(Image.open(q)), img)
+
+
+def test_write_image_round_half_even(tmp_path):
+    from PIL import Image
+    from imagecompression_adversarial_amd import coder
+    # x*255 = 0.5, 1.5, 2.5 -> np.round half-to-even -> 0, 2, 2 (coder.py:45)
+    v = torch.tensor([0.5, 1.5, 2.5, 253.5], dtype=torch.float64) / 255.0
+    x = v.float().view(1, 1, 1, 4).repeat(1, 3, 1, 1)
+    q = tmp_path / "c.png"
+    coder.write_image(x, str(q))
+    got = np.array(Image.open(q))[0, :, 0]
+    ref = np.round(x[0, 0, 0].numpy() * 255.0).astype(np.uint8)  # float32 path as coder.py:45
+    assert np.array_equal(got, ref)
+
+
+def test_model_state_dict_keys():
+    from imagecompression_adversarial_amd import codec
+    m = codec.bmshj2018_hyperprior(1)
+    keys = set(m.state_dict())
+    for k in ("g_a.0.weight", "g_a.1.beta", "g_a.1.gamma", "g_a.1.beta_reparam.pedestal",
+              "g_s.6.bias", "h_a.0.weight", "h_s.4.weight", "entropy_bottleneck._matrix0",
+              "entropy_bottleneck._factor3", "entropy_bottleneck.quantiles", "gaussian_conditional.scale_table"):
+        assert k in keys, k
+    assert m.N == 128 and m.M == 192
+    assert codec.bmshj2018_hyperprior(6).M == 320
+
+
+def test_lr_schedule_matches_torch():
+    from imagecompression_adversarial_amd.attack import _lr_table
+    from oracle.attack import lr_schedule
+    for steps in (1001, 100, 12, 3):
+        assert _lr_table(steps, 0.01) == lr_schedule(steps, 0.01)
