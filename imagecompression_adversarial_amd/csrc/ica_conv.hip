@@ -27,7 +27,7 @@ enum {
   EPI_RELU = 1,      // y = relu(acc + bias)
   EPI_GDN = 2,       // x = acc + bias; y = x * rsqrt(beta' + gamma' x^2)
   EPI_IGDN = 3,      // x = acc + bias; y = x * sqrt(beta' + gamma' x^2)
-  EPI_GDN_BWD = 4,   // acc = dL/dy of a GDN; emit dL/dx  (needs saved x, s)
+  EPI_GDN_BWD = 4,   // acc = dL/dy of a GDN; emit dL/dx  (needs saved y, s)
   EPI_IGDN_BWD = 5,  // same for IGDN
 };
 
@@ -40,7 +40,7 @@ struct ConvParams {
   const float* beta;  // beta' [Cout] (fwd GDN epilogues)
   float* save_x;      // fwd GDN: pre-normalisation activation (optional)
   float* save_s;      // fwd GDN: s = rsqrt(n) | sqrt(n)           (optional)
-  const float* in_x;  // bwd GDN: saved x
+  const float* in_x;  // bwd GDN: saved GDN OUTPUT y = x*s (x is recovered as y/s)
   const float* in_s;  // bwd GDN: saved s
   int N, Cin, Hin, Win, Cout, Hout, Wout;
 };
@@ -148,8 +148,8 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float gx = acc[it][4 * g + e] * xv[e];
           const float s = sv[e];
+          const float gx = acc[it][4 * g + e] * (xv[e] / s);  // in_x holds y = x*s: x = y / s
           tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
         }
       }
@@ -174,7 +174,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
-            v[e] = acc[jt][r] * sv[e] + 2.0f * xv[e] * uacc[r];
+            v[e] = acc[jt][r] * sv[e] + 2.0f * (xv[e] / sv[e]) * uacc[r];
           }
           st4(p.y + o, v);
         }
@@ -420,14 +420,15 @@ __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
 #pragma unroll
     for (int it = 0; it < 3; ++it) acc[it] = f32x16{0};
     const float* wl = p.wp + (size_t)lane * 8;
-    for (int ch = 0; ch < nch; ++ch) {
-      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+    // B (activations, straight from HBM: 32 consecutive pixels x 16 B per plane = 512 B
+    // coalesced) and A (weights, L2) for chunk ch+1 are loaded while chunk ch computes.
+    auto load = [&](int ch, f32x4& v0, f32x4& v1, float (&a)[3][8]) {
+      v0 = f32x4{0.f, 0.f, 0.f, 0.f};
+      v1 = v0;
       if (ok) {
         v0 = ld4(xp + (size_t)(4 * ch + 2 * h) * plane * 4);
         v1 = ld4(xp + (size_t)(4 * ch + 2 * h + 1) * plane * 4);
       }
-      const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      float a[3][8];
 #pragma unroll
       for (int it = 0; it < 3; ++it) {
         const float* wt = wl + ((size_t)it * nch + ch) * 512;
@@ -438,11 +439,26 @@ __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
           a[it][4 + e] = w1[e];
         }
       }
+    };
+    auto compute = [&](const f32x4& v0, const f32x4& v1, const float (&a)[3][8]) {
+      const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 #pragma unroll
-      for (int s = 0; s < 8; ++s)
+      for (int s2 = 0; s2 < 8; ++s2)
 #pragma unroll
-        for (int it = 0; it < 3; ++it) acc[it] = mfma32(a[it][s], b[s], acc[it]);
+        for (int it = 0; it < 3; ++it) acc[it] = mfma32(a[it][s2], b[s2], acc[it]);
+    };
+    f32x4 pa0, pa1, pb0, pb1;
+    float aa[3][8], ab[3][8];
+    load(0, pa0, pa1, aa);
+    int ch = 0;
+#pragma unroll 1
+    for (; ch + 1 < nch; ch += 2) {
+      load(ch + 1, pb0, pb1, ab);
+      compute(pa0, pa1, aa);
+      load(min(ch + 2, nch - 1), pa0, pa1, aa);
+      compute(pb0, pb1, ab);
     }
+    if (ch < nch) compute(pa0, pa1, aa);
     if (q < T3_NPX) {
 #pragma unroll
       for (int it = 0; it < 3; ++it)

@@ -163,9 +163,10 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
     Wo = (W + 2 * (KS // 2) - KS) // S + 1
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
-    sx = ss = None
+    ss = None
     if save and epi in (EPI_GDN, EPI_IGDN):
-        sx = empty_nc4(N, Cout, Ho, Wo, x4.device)
+        # backward needs (y, s): y = x*s is this layer's output (kept alive anyway as the next
+        # layer's input), so only s is written; the bwd epilogue recovers x = y / s.
         ss = empty_nc4(N, Cout, Ho, Wo, x4.device)
     in_x = in_s = None
     if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
@@ -173,9 +174,9 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     ev = _ev_begin(tag)
     call("ica_conv_down", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, KS, S, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
-         ptr(None if gdn is None else gdn.beta), ptr(sx), ptr(ss), ptr(in_x), ptr(in_s), stream())
+         ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), stream())
     _ev_end(ev)
-    return y, sx, ss
+    return y, (y if ss is not None else None), ss
 
 
 def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
@@ -191,9 +192,10 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
         call("ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, stream())
         _ev_end(ev)
         return y, None, None
-    sx = ss = None
+    ss = None
     if save and epi in (EPI_GDN, EPI_IGDN):
-        sx = empty_nc4(N, Cout, Ho, Wo, x4.device)
+        # backward needs (y, s): y = x*s is this layer's output (kept alive anyway as the next
+        # layer's input), so only s is written; the bwd epilogue recovers x = y / s.
         ss = empty_nc4(N, Cout, Ho, Wo, x4.device)
     in_x = in_s = None
     if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
@@ -201,9 +203,9 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     ev = _ev_begin(tag)
     call("ica_conv_up", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
-         ptr(None if gdn is None else gdn.beta), ptr(sx), ptr(ss), ptr(in_x), ptr(in_s), stream())
+         ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), stream())
     _ev_end(ev)
-    return y, sx, ss
+    return y, (y if ss is not None else None), ss
 
 
 # --------------------------------------------------------------------------- #

@@ -129,7 +129,9 @@ def test_gdn_epilogues(K, inverse):
     p = K.PackedConv(w.to(dev()), b.to(dev()), "conv", 2)
     y4, sx, ss = K.conv_down(K.to_nc4(x.to(dev())), C, p.fwd, p.bias, C, 5, 2, epi_f, gd, save=True)
     assert rel_err(K.from_nc4(y4, C).cpu(), ref.detach()) < 2e-5
-    assert rel_err(K.from_nc4(sx, C).cpu(), pre.detach()) < 2e-5
+    assert sx is y4  # saved pair is (GDN output y, s); backward recovers x = y / s
+    # s = n^(-1/2) (GDN) or n^(1/2) (IGDN): y / s reproduces the pre-normalisation x
+    assert rel_err((K.from_nc4(y4, C) / K.from_nc4(ss, C)).cpu(), pre.detach()) < 2e-5
     # backward epilogue: feed g through conv_up of an identity-free weight and compare with
     # autograd of gdn(pre) driven by the same upstream gradient
     g_up = rnd(tuple(ref.shape), 16)
