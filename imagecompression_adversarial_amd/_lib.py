@@ -26,13 +26,13 @@ _sz = C.c_size_t
 _SIGS = {
     "ica_conv_it": [_i],
     "ica_pack_conv_weight_size": [_i, _i, _i, _i],
-    "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _p],
+    "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_up3_size": [_i],
     "ica_pack_up3": [_p, _p, _i, _p],
     "ica_conv_up3": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
-    "ica_conv_down": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
-    "ica_conv_up": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
+    "ica_conv_down": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
+    "ica_conv_up": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "ica_elem_blocks_per_image": [],
     "ica_nchw_to_nc4": [_p, _p, _i, _i, _i, _i, _p],
     "ica_nc4_to_nchw": [_p, _p, _i, _i, _i, _i, _p],
@@ -57,8 +57,22 @@ _SIGS = {
     "ica_avgpool2": [_p, _p, _i, _i, _i, _i, _i, _p],
     "ica_avgpool2_bwd": [_p, _p, _i, _i, _i, _i, _i, _p],
     "ica_scale": [_p, _l, _f, _p],
+    # training side (ica_train.hip)
+    "ica_wgrad_ws_size": [_i, _i, _i, _i],
+    "ica_wgrad_nsplit": [_i, _i, _l],
+    "ica_wgrad": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p],
+    "ica_channel_sum": [_p, _p, _i, _i, _i, _i, _i, _p],
+    "ica_relu_bwd": [_p, _p, _l, _p],
+    "ica_abs_bwd": [_p, _p, _l, _p],
+    "ica_gdn_xsq": [_p, _p, _p, _l, _p],
+    "ica_reparam_bwd": [_p, _p, _p, _l, _f, _i, _p],
+    "ica_bpp_grad": [_p, _p, _l, _f, _p],
+    "ica_gc_bwd": [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_eb_bwd": [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_eb_param_scatter": [_p, _p, _p, _i, _p],
+    "ica_mse_grad": [_p, _p, _p, _i, _i, _i, _f, _p],
 }
-_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_up3_size": _sz}
+_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz}
 
 _lib = None
 

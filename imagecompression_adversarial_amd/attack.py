@@ -7,6 +7,14 @@ PER-IMAGE semantics: image b of the batch follows exactly the trajectory a
 B == 1 reference run would (own loss_i, own branch, own Adam state).  The
 branch `loss_i > -noise` is decided ON DEVICE per image inside the Adam kernel.
 
+``coupled=True`` gives the batch-coupled semantics the adversarial fine-tune
+uses (train.py:342 -> attack_rd.py:333-334, adv_train.py:146-155): loss_i is
+the mean over the WHOLE batch and one branch is taken for all images.  With a
+process group the batch is the union of every rank's shard: the per-image
+loss_i are summed across ranks by one 4-byte-per-rank all-reduce per step
+(RCCL on the GPU box), and all gradients are normalised by the global image
+count, so N ranks reproduce one B_global run.
+
 ``ifgsm_batch`` == attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438) without
 random start (the reference default path), per image.
 """
@@ -17,6 +25,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from . import dist as D
 from . import hip_ops as K
 from . import msssim as MS
 from ._lib import call, ptr, stream
@@ -91,7 +100,7 @@ class AttackLoop:
     """Holds the device state of one batched attack_rd.attack_ run."""
 
     def __init__(self, kern: CodecKernels, im_s: torch.Tensor, steps=1001, epsilon=16.0, noise_thr=1e-4,
-                 lr=0.01, att_metric="L2", clamp=True, init_noise=None):
+                 lr=0.01, att_metric="L2", clamp=True, init_noise=None, coupled=False, group=None):
         if att_metric not in ("L2", "ms-ssim"):
             raise ValueError(f"att_metric {att_metric!r} not supported (reference: L2, ms-ssim)")
         self.kern = kern
@@ -102,6 +111,11 @@ class AttackLoop:
         self.steps, self.eps, self.thr = steps, float(epsilon) / 255.0, float(noise_thr)
         self.metric, self.clamp = att_metric, clamp
         self.invN = float(1.0 / (3 * H * W))  # torch: grad / numel in fp32
+        self.coupled, self.group = coupled, group
+        self.B_global = D.global_count(B, im_s.device, group) if coupled else B
+        # gradient scale of the mean-type losses: per image (1/numel) or over the whole batch
+        self.gscale = float(1.0 / (self.B_global * 3 * H * W)) if coupled else self.invN
+        self.dval = 1.0 / self.B_global if coupled else 1.0
         dev = im_s.device
         self.noise = torch.zeros_like(self.im_s) if init_noise is None else init_noise.clone().contiguous()
         self.m = torch.zeros_like(self.im_s)
@@ -134,12 +148,12 @@ class AttackLoop:
         del y4
         if self.metric == "L2":
             call("ica_attack_loss", ptr(xh4), ptr(self.output_s), ptr(self.grad4), ptr(self.part), B, H, W,
-                 self.invN, int(self.clamp), 0, stream())
+                 self.gscale, int(self.clamp), 0, stream())
         else:
             # loss_o = ms_ssim(out, output_s) per image (attack_rd.py:362)
             out = torch.empty_like(self.im_s)
             call("ica_nc4_bound_to_nchw", ptr(xh4), ptr(out), B, H, W, int(self.clamp), stream())
-            ones = torch.ones(B, device=out.device)
+            ones = torch.full((B,), self.dval, device=out.device)
             _, gout, _ = MS.ms_ssim_value_and_grad(out, self.output_s, ones)
             call("ica_bound_bwd_nc4", ptr(xh4), ptr(gout), ptr(self.grad4), B, H, W, int(self.clamp), stream())
         gy4 = kern.g_s_backward(self.grad4, ss)
@@ -151,18 +165,20 @@ class AttackLoop:
         call("ica_attack_prologue", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
              self.eps, stream())
         K.reduce_rows(self.part, B, self.invN, out=self.loss_i)
+        if self.coupled:
+            D.couple_loss_i(self.loss_i, self.B_global, self.group)
         gx4 = self.network_grad()
         cheap_grad = None
         if self.metric == "ms-ssim":
             # cheap branch loss = 1 - ms_ssim(im_s, im_in): d/d im_in = -dMS/dY
             im_in = torch.empty_like(self.im_s)
             call("ica_nc4_bound_to_nchw", ptr(self.im_in4), ptr(im_in), B, H, W, 0, stream())
-            _, _, gY = MS.ms_ssim_value_and_grad(self.im_s, im_in, -torch.ones(B, device=im_in.device))
+            _, _, gY = MS.ms_ssim_value_and_grad(self.im_s, im_in, torch.full((B,), -self.dval, device=im_in.device))
             cheap_grad = gY
         bc2s, neg_step = self._adam_scalars(i)
         call("ica_attack_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(cheap_grad),
              ptr(self.m), ptr(self.v), ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr,
-             self.invN, bc2s, neg_step, ptr(self.branch), stream())
+             self.gscale, bc2s, neg_step, ptr(self.branch), stream())
         if census:
             return self.branch.tolist()
         return None
@@ -177,8 +193,9 @@ class AttackLoop:
 
 
 def attack_batch(kern: CodecKernels, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
-                 clamp=True, init_noise=None, eval_msssim=True, record=False) -> AttackResult:
-    loop = AttackLoop(kern, im_s, steps, epsilon, noise_thr, lr, att_metric, clamp, init_noise)
+                 clamp=True, init_noise=None, eval_msssim=True, record=False, coupled=False,
+                 group=None) -> AttackResult:
+    loop = AttackLoop(kern, im_s, steps, epsilon, noise_thr, lr, att_metric, clamp, init_noise, coupled, group)
     branches = loop.run(record=record)
     im_, out, bpp, mse_in, mse_out, msim_in, msim_out, vi, vi_msim = evaluate(
         kern, loop.im_in, loop.im_s, loop.output_s, clamp, adv=False, msssim=eval_msssim)

@@ -43,6 +43,7 @@ struct ConvParams {
   const float* in_x;  // bwd GDN: saved GDN OUTPUT y = x*s (x is recovered as y/s)
   const float* in_s;  // bwd GDN: saved s
   int N, Cin, Hin, Win, Cout, Hout, Wout;
+  float* save_t;      // bwd GDN (training): dL/dn per element, for the GDN parameter gradients
 };
 
 // --------------------------------------------------------------------------
@@ -152,6 +153,9 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const float gx = acc[it][4 * g + e] * (xv[e] / s);  // in_x holds y = x*s: x = y / s
           tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
         }
+        if (p.save_t && valid)
+          st4(p.save_t + off(it * 8 + 2 * g + h),
+              f32x4{tt[it][4 * g], tt[it][4 * g + 1], tt[it][4 * g + 2], tt[it][4 * g + 3]});
       }
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) {
@@ -186,6 +190,14 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 // Load one (chunk, tap) weight fragment set: IT tiles x KH floats per lane.
 template <int IT, int KH>
 ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
+#ifdef ICA_ABLATE_WLOAD
+  // timing-only build: no weight traffic (wrong results)
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int e = 0; e < KH; ++e) a[it][e] = __builtin_bit_cast(float, (int)((threadIdx.x + it * 7 + e + (int)(size_t)w) & 0x3f) | 0x3c000000);
+  return;
+#endif
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     if constexpr (KH == 8) {
@@ -249,7 +261,11 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
         const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
         const int c4 = ch * NQ + q, iy = iy0 + pr, ix = ix0 + pc;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#ifdef ICA_ABLATE_FILL
+        if (false) {
+#else
         if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
+#endif
           v = ld4(p.x + ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4);
           if constexpr (CC == 4) {
 #pragma unroll
@@ -527,7 +543,7 @@ __global__ void pack_up3_kernel(const float* __restrict__ w, float* __restrict__
 //   o = cb*IT*32 + it*32 + (lane&31) ; c = chunk*CC + (lane>>5)*KH + s
 // value = w[o*so + c*sc + ky*KS + kx]  (0 outside O x C)
 __global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict__ dst, int O, int C, int KS,
-                                 long so, long sc, int IT, int CC, int order, long total) {
+                                 long so, long sc, int IT, int CC, int order, long total, int flip) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int KH = CC / 2, KK = KS * KS;
@@ -545,7 +561,8 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict_
   const int o = cb * IT * 32 + it * 32 + (lane & 31);
   const int c = chunk * CC + (lane >> 5) * KH + s;
   float v = 0.f;
-  if (o < O && c < C) v = w[o * so + c * sc + (tap / KS) * KS + (tap % KS)];
+  const int wt = flip ? KK - 1 - tap : tap;  // flip: spatially reversed kernel (dgrad of a stride-1 conv)
+  if (o < O && c < C) v = w[o * so + c * sc + (wt / KS) * KS + (wt % KS)];
   dst[i] = v;
 }
 
@@ -682,11 +699,11 @@ size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC) {
 }
 
 int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long so, long sc, int CC, int order,
-                         hipStream_t st) {
+                         int flip, hipStream_t st) {
   const int IT = ica_conv_it(O);
   const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC);
   hipLaunchKernelGGL(pack_conv_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc, IT, CC,
-                     order, total);
+                     order, total, flip);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -707,7 +724,7 @@ int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, i
                  hipStream_t st) {
   if (Cin % 16 != 0) return -2;
   ConvParams p{x, y, wp, bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, Cin, Hin, Win, 3,
-               2 * Hin, 2 * Win};
+               2 * Hin, 2 * Win, nullptr};
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
   hipLaunchKernelGGL(conv_up3_kernel, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
@@ -726,8 +743,9 @@ int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_e
 
 int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
                   int Cout, int Hout, int Wout, int KS, int S, int epi, const float* gp, const float* beta,
-                  float* save_x, float* save_s, const float* in_x, const float* in_s, hipStream_t st) {
-  ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout};
+                  float* save_x, float* save_s, const float* in_x, const float* in_s, float* save_t,
+                  hipStream_t st) {
+  ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout, save_t};
   const int it = ica_conv_it(Cout);
   if (epi >= EPI_GDN && Cout != it * 32) return -4;
   if (KS == 5 && S == 2) return pick_epi_down<5, 2>(p, it, epi, st);
@@ -737,8 +755,8 @@ int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, 
 
 int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
                 int Cout, int Hout, int Wout, int epi, const float* gp, const float* beta, float* save_x,
-                float* save_s, const float* in_x, const float* in_s, hipStream_t st) {
-  ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout};
+                float* save_s, const float* in_x, const float* in_s, float* save_t, hipStream_t st) {
+  ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout, save_t};
   const int it = ica_conv_it(Cout);
   if (epi >= EPI_GDN && Cout != it * 32) return -4;
   return pick_up(p, it, epi, st);

@@ -75,13 +75,14 @@ def from_nc4(x4: torch.Tensor, C: int) -> torch.Tensor:
 # --------------------------------------------------------------------------- #
 # Weight packing
 # --------------------------------------------------------------------------- #
-def pack_conv(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order: int, CC: int) -> torch.Tensor:
-    """Pack a conv weight viewed as W[o][c][ky][kx] (strides so, sc; k contiguous)."""
+def pack_conv(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order: int, CC: int,
+              flip: bool = False) -> torch.Tensor:
+    """Pack a conv weight viewed as W[o][c][ky][kx] (strides so, sc; k contiguous); flip reverses the taps."""
     w = w.detach().contiguous()
     _dev_check(w, "weight")
     n = int(lib().ica_pack_conv_weight_size(O, Cc, KS, CC))
     dst = torch.empty(n, dtype=torch.float32, device=w.device)
-    call("ica_pack_conv_weight", ptr(w), ptr(dst), O, Cc, KS, so, sc, CC, order, stream())
+    call("ica_pack_conv_weight", ptr(w), ptr(dst), O, Cc, KS, so, sc, CC, order, int(flip), stream())
     return dst
 
 
@@ -116,9 +117,12 @@ class PackedConv:
             # forward: o = co, c = ci
             self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
                                  conv_cc(self.Cin))
-            # dgrad (conv_up): o = ci, c = co   (only k5 s2 layers have a dgrad path)
+            # dgrad: k5 s2 -> conv_up (o = ci, c = co); k3 s1 -> conv_down with the taps reversed
             self.bwd = None
-            if self.KS == 5 and stride == 2 and self.Cout % 16 == 0:
+            if self.KS == 3 and stride == 1 and self.Cout % 16 == 0:
+                self.bwd = pack_conv(weight, self.Cin, self.Cout, 3, KK, self.Cin * KK, ORDER_DOWN,
+                                     conv_cc(self.Cout), flip=True)
+            elif self.KS == 5 and stride == 2 and self.Cout % 16 == 0:
                 if self.Cin == 3:   # input-gradient of the first conv: Z-gather kernel
                     self.bwd = pack_up3(weight)
                 else:
@@ -157,8 +161,9 @@ class PackedGDN:
 # Convolutions
 # --------------------------------------------------------------------------- #
 def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False,
-              saved=None, out=None, tag=None):
-    """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s)."""
+              saved=None, out=None, tag=None, save_t=None):
+    """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s).
+    save_t: optional nChw4c output of t = dL/dn for the GDN-bwd epilogues (GDN parameter gradients)."""
     N, _, H, W, _ = x4.shape
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
     Wo = (W + 2 * (KS // 2) - KS) // S + 1
@@ -174,13 +179,13 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     ev = _ev_begin(tag)
     call("ica_conv_down", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, KS, S, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
-         ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), stream())
+         ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), ptr(save_t), stream())
     _ev_end(ev)
     return y, (y if ss is not None else None), ss
 
 
 def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
-            out=None, tag=None):
+            out=None, tag=None, save_t=None):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
     Ho, Wo = 2 * H, 2 * W
@@ -203,7 +208,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     ev = _ev_begin(tag)
     call("ica_conv_up", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
-         ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), stream())
+         ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), ptr(save_t), stream())
     _ev_end(ev)
     return y, (y if ss is not None else None), ss
 
@@ -285,3 +290,84 @@ def gc_likelihood(y4: torch.Tensor, C: int, scales4: torch.Tensor, means4=None, 
 
 def bits_to_bpp(sumlog: torch.Tensor, num_pixels: int) -> torch.Tensor:
     return sumlog / (-math.log(2) * num_pixels)
+
+
+# --------------------------------------------------------------------------- #
+# Training-side wrappers (ica_train.hip)
+# --------------------------------------------------------------------------- #
+def wgrad(Sm4, A, Lg4, Bc, KS, S, out, accumulate=False):
+    """out[a][b][ky][kx] (+)= sum Sm[n][a][p] Lg[n][b][S p + k - KS//2]  (see include/ica_hip.h)."""
+    N, _, Hs, Ws, _ = Sm4.shape
+    _, _, Hb, Wb, _ = Lg4.shape
+    if out.numel() != A * Bc * KS * KS or not out.is_contiguous():
+        raise RuntimeError("wgrad: output must be a contiguous [A][B][KS][KS] tensor")
+    nsplit = int(lib().ica_wgrad_nsplit(A, Bc, N * Hs * ((Ws + 31) // 32)))
+    ws = torch.empty(int(lib().ica_wgrad_ws_size(A, Bc, KS, nsplit)), device=Sm4.device)
+    call("ica_wgrad", ptr(Sm4), ptr(Lg4), ptr(ws), ptr(out), N, A, Bc, Hs, Ws, Hb, Wb, KS, S, KS // 2, nsplit,
+         int(accumulate), stream())
+    return out
+
+
+def channel_sum(x4, C, out, accumulate=False):
+    N, _, H, W, _ = x4.shape
+    call("ica_channel_sum", ptr(x4), ptr(out), N, C, H, W, int(accumulate), stream())
+    return out
+
+
+def relu_bwd_(g4, y4):
+    call("ica_relu_bwd", ptr(g4), ptr(y4), g4.numel(), stream())
+    return g4
+
+
+def abs_bwd_(g4, x4):
+    call("ica_abs_bwd", ptr(g4), ptr(x4), g4.numel(), stream())
+    return g4
+
+
+def gdn_xsq(y4, s4):
+    out = torch.empty_like(y4)
+    call("ica_gdn_xsq", ptr(y4), ptr(s4), ptr(out), y4.numel(), stream())
+    return out
+
+
+def reparam_bwd(p, gprime, gout, bound, accumulate=True):
+    call("ica_reparam_bwd", ptr(p.detach().contiguous()), ptr(gprime.contiguous()), ptr(gout), p.numel(),
+         float(bound), int(accumulate), stream())
+
+
+def bpp_grad(lik4, scale):
+    g = torch.empty_like(lik4)
+    call("ica_bpp_grad", ptr(lik4), ptr(g), lik4.numel(), float(scale), stream())
+    return g
+
+
+def gc_bwd(yt4, sigma4, gl4, C):
+    N, _, H, W, _ = yt4.shape
+    gy, gs = torch.empty_like(yt4), torch.empty_like(yt4)
+    call("ica_gc_bwd", ptr(yt4), ptr(sigma4), ptr(gl4), ptr(gy), ptr(gs), N, C, H, W, stream())
+    return gy, gs
+
+
+def eb_bwd(v4, gl4, eb: PackedEB, C):
+    N, _, H, W, _ = v4.shape
+    gv = torch.zeros_like(v4)
+    gprm = torch.empty(C * 58, device=v4.device)
+    call("ica_eb_bwd", ptr(v4), ptr(gl4), ptr(eb.prm), ptr(gv), ptr(gprm), N, C, H, W, stream())
+    return gv, gprm
+
+
+def eb_param_scatter(gprm, raw: list, graw: list, C):
+    """Accumulate the 58-per-channel effective-parameter grads into the 14 raw EB parameter grads."""
+    import ctypes as Cc
+    for t in list(raw) + list(graw):
+        if not t.is_contiguous():
+            raise RuntimeError("entropy_bottleneck params/grads must be contiguous")
+    ra = (Cc.c_void_p * 14)(*[t.data_ptr() for t in raw])
+    ga = (Cc.c_void_p * 14)(*[t.data_ptr() for t in graw])
+    call("ica_eb_param_scatter", ptr(gprm), Cc.cast(ra, Cc.c_void_p), Cc.cast(ga, Cc.c_void_p), C, stream())
+
+
+def mse_grad_(xh4, x, g4, scale):
+    B, _, H, W = x.shape
+    call("ica_mse_grad", ptr(xh4), ptr(x.contiguous()), ptr(g4), B, H, W, float(scale), stream())
+    return g4

@@ -44,9 +44,10 @@ enum { ICA_EPI_BIAS = 0, ICA_EPI_RELU = 1, ICA_EPI_GDN = 2, ICA_EPI_IGDN = 3, IC
 int ica_conv_it(int cout);
 /* floats needed for the packed fragments of a weight viewed as W[O][C][KS][KS], chunk CC (4|16). */
 size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC);
-/* Pack W (element (o,c,ky,kx) at w[o*so + c*sc + ky*KS + kx]); order 0 = conv_down, 1 = conv_up. */
+/* Pack W (element (o,c,ky,kx) at w[o*so + c*sc + ky*KS + kx]); order 0 = conv_down, 1 = conv_up.
+ * flip != 0 reverses the taps (W[o][c][KS-1-ky][KS-1-kx]): the dgrad of a stride-1 conv as a conv_down. */
 int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long so, long sc, int CC, int order,
-                         hipStream_t stream);
+                         int flip, hipStream_t stream);
 /* GDN reparametrisation + fragment packing: gamma' = max(gamma,2^-18)^2 - 2^-36 (transpose 0: gamma', 1: gamma'^T),
  * beta_eff = max(beta, beta_bound)^2 - 2^-36.  gp holds (C/32)^2 * 1024 floats. */
 int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_eff, int C, int transpose,
@@ -57,11 +58,14 @@ int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_e
  * gp = gamma'^T fragments, in_x/in_s = the saved x/s of that GDN; y receives dL/dx. */
 int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
                   int Cout, int Hout, int Wout, int KS, int S, int epi, const float* gp, const float* beta,
-                  float* save_x, float* save_s, const float* in_x, const float* in_s, hipStream_t stream);
-/* y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+ epilogue); Cin % 16 == 0. */
+                  float* save_x, float* save_s, const float* in_x, const float* in_s, float* save_t,
+                  hipStream_t stream);
+/* y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+ epilogue); Cin % 16 == 0.
+ * save_t (GDN_BWD/IGDN_BWD only, may be NULL): receives t = dL/dn, n = beta' + gamma' x^2 the GDN norm
+ * (nChw4c), from which the GDN parameter gradients follow (ica_channel_sum, ica_wgrad KS=1). */
 int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
                 int Cout, int Hout, int Wout, int epi, const float* gp, const float* beta, float* save_x,
-                float* save_s, const float* in_x, const float* in_s, hipStream_t stream);
+                float* save_s, const float* in_x, const float* in_s, float* save_t, hipStream_t stream);
 /* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
 size_t ica_pack_up3_size(int Cin);
 int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t stream);
@@ -111,6 +115,42 @@ int ica_msssim_combine(const float* lvl, int P, int G, int mode, const float* dv
 int ica_avgpool2(const float* X, float* Y, int P, int H, int W, int ph, int pw, hipStream_t stream);
 int ica_avgpool2_bwd(const float* gO, float* gX, int P, int H, int W, int ph, int pw, hipStream_t stream);
 int ica_scale(float* x, long n, float s, hipStream_t stream);
+
+
+/* ---- adversarial fine-tune backward (ica_train.hip) ------------------------
+ * Replaces the autograd backward of `out_criterion["loss"].backward()` in train.py:358-359 (train.train --adv),
+ * adv_train.py:184-186, for the bmshj2018 models; RateDistortionLoss train.py:37-96. */
+/* floats of split-K workspace ica_wgrad needs; ica_wgrad_nsplit picks the split count for nchunks pixel rows. */
+size_t ica_wgrad_ws_size(int A, int Bc, int KS, int nsplit);
+int ica_wgrad_nsplit(int A, int Bc, long nchunks);
+/* out[a][b][ky][kx] (+)= sum_{n,p} Sm[n][a][p] * Lg[n][b][S*p + k - P]   (nChw4c operands)
+ *   conv   W[o][c]:  Sm = dL/dy (a = o, small grid = output), Lg = x (b = c, big grid = input)
+ *   deconv W[c][o]:  Sm = x (a = c, small grid = input),      Lg = dL/dy (b = o, big grid = output)
+ * KS,S in {(5,2),(3,1),(1,1)}; deterministic (fixed-order split reduction). */
+int ica_wgrad(const float* Sm, const float* Lg, float* ws, float* out, int N, int A, int Bc, int Hs, int Ws, int Hb,
+              int Wb, int KS, int S, int P, int nsplit, int accumulate, hipStream_t stream);
+/* out[c] (+)= sum over n, pixels of x (nChw4c): bias and GDN beta' gradients. */
+int ica_channel_sum(const float* x, float* out, int N, int C, int H, int W, int accumulate, hipStream_t stream);
+int ica_relu_bwd(float* g, const float* y, long n, hipStream_t stream);          /* g *= (y > 0) */
+int ica_abs_bwd(float* g, const float* x, long n, hipStream_t stream);           /* g *= sign(x) */
+int ica_gdn_xsq(const float* y, const float* s, float* out, long n, hipStream_t stream); /* (y/s)^2 */
+/* NonNegativeParametrizer backward (utils/ops.py:58-81): gout (+)= g' * 2 max(p,bound), LowerBound gate. */
+int ica_reparam_bwd(const float* p, const float* gprime, float* gout, long n, float bound, int accumulate,
+                    hipStream_t stream);
+/* d/dlik of sum log(clamp(lik, 2^-16)) * scale  (train.py:60-64). */
+int ica_bpp_grad(const float* lik, float* g, long n, float scale, hipStream_t stream);
+/* GaussianConditional backward (train mode, no means): gy = dL/dy_tilde, gs = dL/dscales. */
+int ica_gc_bwd(const float* y_tilde, const float* sigma, const float* glik, float* gy, float* gs, int B, int C, int H,
+               int W, hipStream_t stream);
+/* EntropyBottleneck backward (train mode): gv = dL/dz_tilde; gprm[C][58] = grads of the effective params. */
+int ica_eb_bwd(const float* v, const float* glik, const float* prm, float* gv, float* gprm, int N, int C, int H, int W,
+               hipStream_t stream);
+/* gprm -> raw parameter grads (softplus / tanh chains); raw, graw: host arrays of 14 device pointers
+ * (_matrix0..4, _bias0..4, _factor0..3); graw is accumulated into. */
+int ica_eb_param_scatter(const float* gprm, const float* const* raw, float* const* graw, int C, hipStream_t stream);
+/* g4 += scale * (x_hat - x)   (x_hat nChw4c 3 channels, x NCHW). */
+int ica_mse_grad(const float* x_hat4, const float* x, float* g4, int B, int H, int W, float scale,
+                 hipStream_t stream);
 
 #ifdef __cplusplus
 }

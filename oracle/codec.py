@@ -175,7 +175,9 @@ def eb_likelihood(P, v, prefix="entropy_bottleneck"):
     upper = eb_logits_cumulative(P, v + 0.5, prefix)
     sign = -torch.sign(lower + upper)
     lik = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))
-    return torch.clamp(lik, min=LIKELIHOOD_BOUND)
+    # CompressAI likelihood_lower_bound = LowerBound(1e-9): clamp forward, one-sided pass-through backward
+    # (identical rule to utils/ops.py:28-41)
+    return LowBound.apply(lik, LIKELIHOOD_BOUND)
 
 
 def entropy_bottleneck(P, z, training=False, noise=None, prefix="entropy_bottleneck"):
@@ -214,11 +216,13 @@ def _std_cumulative(x):
 
 def gc_likelihood(y_hat, scales, means=None):
     values = y_hat - means if means is not None else y_hat
-    scales = torch.clamp(scales, min=SCALE_BOUND)
+    # lower_bound_scale = LowerBound(0.11) and LowerBound(1e-9) on the likelihood:
+    # same forward as a clamp, but the gradient passes where it would push the value up (g < 0)
+    scales = LowBound.apply(scales, SCALE_BOUND)
     values = torch.abs(values)
     upper = _std_cumulative((0.5 - values) / scales)
     lower = _std_cumulative((-0.5 - values) / scales)
-    return torch.clamp(upper - lower, min=LIKELIHOOD_BOUND)
+    return LowBound.apply(upper - lower, LIKELIHOOD_BOUND)
 
 
 def gaussian_conditional(y, scales, means=None, training=False, noise=None):

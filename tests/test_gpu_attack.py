@@ -82,6 +82,33 @@ def test_attack_vs_oracle_256(hyper3):
     assert torch.allclose(res.msim_out.cpu(), ref.eval.msim_out, rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("thr", [1e-4, 3e-5])
+def test_coupled_attack_vs_oracle(hyper3, thr):
+    """Batch-coupled semantics (train.py:342 -> attack_rd.py:333-334): one branch for the batch, batch-mean
+    losses.  Same branch sequence as the oracle, noise rel <= 2e-3."""
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = hyper3
+    x = rnd((3, 3, 64, 128), 51)
+    res = attack_batch(kern, x.to(DEV), steps=8, noise_thr=thr, coupled=True, eval_msssim=False, record=True)
+    rec = []
+    ref = oatt.attack(P, x, steps=8, noise_thr=thr, coupled=True, eval_msssim=False, record=rec)
+    for i, br in enumerate(res.branches):
+        assert len(set(br)) == 1, (i, br)
+        assert bool(br[0]) == bool(rec[i]["cheap"][0]), i
+    assert rel_err(res.noise.cpu(), ref.noise) < 2e-3
+    assert rel_err(res.im_adv.cpu(), ref.im_adv) < 1e-5
+
+
+def test_coupled_ms_ssim_attack_vs_oracle(hyper3):
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = hyper3
+    x = rnd((2, 3, 192, 192), 53)
+    res = attack_batch(kern, x.to(DEV), steps=3, att_metric="ms-ssim", coupled=True, eval_msssim=False)
+    ref = oatt.attack(P, x, steps=3, att_metric="ms-ssim", coupled=True, eval_msssim=False)
+    d = (res.noise.cpu() - ref.noise).abs() / ref.noise.abs().max()
+    assert float(d.max()) < 2e-2 and float((d < 1e-3).float().mean()) > 0.999
+
+
 def test_batch_independence_bitexact(hyper3):
     from imagecompression_adversarial_amd.attack import attack_batch
     P, kern = hyper3
