@@ -25,8 +25,9 @@ _sz = C.c_size_t
 # name -> argtypes (restype int unless listed in _RESTYPES)
 _SIGS = {
     "ica_conv_it": [_i],
-    "ica_pack_conv_weight_size": [_i, _i, _i, _i],
-    "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _p],
+    "ica_pack_conv_weight_size": [_i, _i, _i, _i, _i],
+    "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _i, _p],
+    "ica_conv_ex": [_p, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_up3_size": [_i],
     "ica_pack_up3": [_p, _p, _i, _p],
@@ -46,6 +47,7 @@ _SIGS = {
     "ica_eb_likelihood": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_pack_eb": [_p, _p, _p, _i, _p],
     "ica_abs": [_p, _p, _l, _p],
+    "ica_round": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],
     "ica_nc4_bound_to_nchw": [_p, _p, _i, _i, _i, _i, _p],
@@ -73,6 +75,16 @@ _SIGS = {
     "ica_mse_grad": [_p, _p, _p, _i, _i, _i, _f, _p],
 }
 _RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz}
+
+
+
+class ConvArgs(C.Structure):
+    """include/ica_hip.h ica_conv_args."""
+    _fields_ = ([(n, C.c_void_p) for n in ("x", "y", "wp", "bias", "gp", "beta", "save_x", "save_s", "in_x", "in_s",
+                                            "save_t", "res", "mask")]
+                + [(n, C.c_int) for n in ("N", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kind", "KS", "S", "epi",
+                                           "it", "fill_mode", "ps")])
+
 
 _lib = None
 

@@ -17,9 +17,11 @@ def init_model(MODEL, quality, metric, pretrained=True):
         return codec.bmshj2018_factorized(quality=quality, metric=metric, pretrained=pretrained)
     if MODEL == "hyper":
         return codec.bmshj2018_hyperprior(quality=quality, metric=metric, pretrained=pretrained)
-    if MODEL in ("context", "cheng2020", "debug"):
-        raise NotImplementedError(f"model '{MODEL}' is not on this backend yet (SURVEY §8f / a17); "
-                                  "supported: factorized, hyper")
+    if MODEL == "cheng2020":
+        return codec.cheng2020_anchor(quality=quality, metric=metric, pretrained=pretrained)
+    if MODEL in ("context", "debug"):
+        raise NotImplementedError(f"model '{MODEL}' is not on this backend (out of §8 scope); "
+                                  "supported: factorized, hyper, cheng2020")
     raise AssertionError(f"'{MODEL}' not in ['factorized', 'hyper', 'context', 'cheng2020', 'debug']")
 
 
@@ -39,6 +41,15 @@ def entropy_estimator(y, net, MODEL):
         z_hat, z_likelihoods = net.entropy_bottleneck(z)
         scales_hat = net.h_s(z_hat)
         y_hat, y_likelihoods = net.gaussian_conditional(y, scales_hat)
+    elif MODEL in ("context", "cheng2020"):
+        z = net.h_a(y)
+        z_hat, z_likelihoods = net.entropy_bottleneck(z)
+        params = net.h_s(z_hat)
+        y_hat = net.gaussian_conditional.quantize(y, "noise" if net.training else "dequantize")
+        ctx_params = net.context_prediction(y_hat)
+        gaussian_params = net.entropy_parameters(torch.cat((params, ctx_params), dim=1))
+        scales_hat, means_hat = gaussian_params.chunk(2, 1)
+        _, y_likelihoods = net.gaussian_conditional(y, scales_hat, means=means_hat)
     else:
         raise NotImplementedError(MODEL)
     return y_hat, z_hat, {"y": y_likelihoods, "z": z_likelihoods}
@@ -52,5 +63,15 @@ def probe(x, net, name="y_hat", MODEL="hyper"):
     if name == "scales_hat":
         return net.h_s(net.h_a(net.g_a(x)))
     if name == "means_hat":
+        if MODEL in ("context", "cheng2020"):
+            y = net.g_a(x)
+            z = net.h_a(y)
+            y_hat = net.gaussian_conditional.quantize(y, "noise" if net.training else "dequantize")
+            z_hat, _ = net.entropy_bottleneck(z)
+            params = net.h_s(z_hat)
+            ctx_params = net.context_prediction(y_hat)
+            gaussian_params = net.entropy_parameters(torch.cat((params, ctx_params), dim=1))
+            _, means_hat = gaussian_params.chunk(2, 1)
+            return means_hat
         return None
     raise ValueError(name)

@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import engine as E
+from . import engine_cheng as EC
 from . import hip_ops as K
 
 # --------------------------------------------------------------------------- #
@@ -215,6 +216,144 @@ class HyperSynthesisTransform(_ForwardOnly):
 
 
 # --------------------------------------------------------------------------- #
+# cheng2020-anchor layers (compressai.layers)
+# --------------------------------------------------------------------------- #
+def conv3x3(in_ch, out_ch, stride=1):
+    return nn.Conv2d(in_ch, out_ch, kernel_size=3, stride=stride, padding=1)
+
+
+def conv1x1(in_ch, out_ch, stride=1):
+    return nn.Conv2d(in_ch, out_ch, kernel_size=1, stride=stride)
+
+
+def subpel_conv3x3(in_ch, out_ch, r=1):
+    return nn.Sequential(nn.Conv2d(in_ch, out_ch * r ** 2, kernel_size=3, padding=1), nn.PixelShuffle(r))
+
+
+class _FusedOnly(nn.Module):
+    def forward(self, x):
+        raise RuntimeError(f"{type(self).__name__} runs fused inside its transform on this backend")
+
+
+class ResidualBlockWithStride(_FusedOnly):
+    def __init__(self, in_ch, out_ch, stride=2):
+        super().__init__()
+        self.conv1 = conv3x3(in_ch, out_ch, stride=stride)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = conv3x3(out_ch, out_ch)
+        self.gdn = GDN(out_ch)
+        self.skip = conv1x1(in_ch, out_ch, stride=stride) if (stride != 1 or in_ch != out_ch) else None
+
+
+class ResidualBlockUpsample(_FusedOnly):
+    def __init__(self, in_ch, out_ch, upsample=2):
+        super().__init__()
+        self.subpel_conv = subpel_conv3x3(in_ch, out_ch, upsample)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv = conv3x3(out_ch, out_ch)
+        self.igdn = GDN(out_ch, inverse=True)
+        self.upsample = subpel_conv3x3(in_ch, out_ch, upsample)
+
+
+class ResidualBlock(_FusedOnly):
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.conv1 = conv3x3(in_ch, out_ch)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = conv3x3(out_ch, out_ch)
+        self.skip = conv1x1(in_ch, out_ch) if in_ch != out_ch else None
+
+
+class ChengAnalysisTransform(_FusedSequential):
+    def __init__(self, N):
+        super().__init__(ResidualBlockWithStride(3, N, 2), ResidualBlock(N, N), ResidualBlockWithStride(N, N, 2),
+                         ResidualBlock(N, N), ResidualBlockWithStride(N, N, 2), ResidualBlock(N, N),
+                         conv3x3(N, N, stride=2))
+        self.out_channels = N
+
+    def _make_executor(self, sd):
+        return EC.ChengAnalysis(sd, prefix="")
+
+
+class ChengSynthesisTransform(_FusedSequential):
+    def __init__(self, N):
+        super().__init__(ResidualBlock(N, N), ResidualBlockUpsample(N, N, 2), ResidualBlock(N, N),
+                         ResidualBlockUpsample(N, N, 2), ResidualBlock(N, N), ResidualBlockUpsample(N, N, 2),
+                         ResidualBlock(N, N), subpel_conv3x3(N, 3, 2))
+        self.out_channels = 3
+
+    def _make_executor(self, sd):
+        return EC.ChengSynthesis(sd, prefix="")
+
+
+class ChengHyperAnalysis(_ForwardOnly):
+    def __init__(self, N):
+        super().__init__(conv3x3(N, N), nn.LeakyReLU(inplace=True), conv3x3(N, N), nn.LeakyReLU(inplace=True),
+                         conv3x3(N, N, stride=2), nn.LeakyReLU(inplace=True), conv3x3(N, N),
+                         nn.LeakyReLU(inplace=True), conv3x3(N, N, stride=2))
+        self.out_channels = N
+
+    def _make_executor(self, sd):
+        return EC.ChengHA(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4)
+
+
+class ChengHyperSynthesis(_ForwardOnly):
+    def __init__(self, N):
+        super().__init__(conv3x3(N, N), nn.LeakyReLU(inplace=True), subpel_conv3x3(N, N, 2),
+                         nn.LeakyReLU(inplace=True), conv3x3(N, N * 3 // 2), nn.LeakyReLU(inplace=True),
+                         subpel_conv3x3(N * 3 // 2, N * 3 // 2, 2), nn.LeakyReLU(inplace=True),
+                         conv3x3(N * 3 // 2, N * 2))
+        self.out_channels = 2 * N
+
+    def _make_executor(self, sd):
+        return EC.ChengHS(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4)
+
+
+class EntropyParameters(_ForwardOnly):
+    def __init__(self, M):
+        super().__init__(nn.Conv2d(M * 12 // 3, M * 10 // 3, 1), nn.LeakyReLU(inplace=True),
+                         nn.Conv2d(M * 10 // 3, M * 8 // 3, 1), nn.LeakyReLU(inplace=True),
+                         nn.Conv2d(M * 8 // 3, M * 6 // 3, 1))
+        self.out_channels = M * 6 // 3
+
+    def _make_executor(self, sd):
+        return EC.ChengEntropyParameters(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4)
+
+
+class MaskedConv2d(nn.Conv2d):
+    """compressai.layers.MaskedConv2d (type 'A' context model), forward on the HIP conv engine."""
+
+    def __init__(self, *args, mask_type="A", **kwargs):
+        super().__init__(*args, **kwargs)
+        if mask_type not in ("A", "B"):
+            raise ValueError(f'Invalid "mask_type" value "{mask_type}"')
+        self.mask_type = mask_type
+        self.register_buffer("mask", torch.ones_like(self.weight.data))
+        _, _, h, w = self.mask.size()
+        self.mask[:, :, h // 2, w // 2 + (mask_type == "B"):] = 0
+        self.mask[:, :, h // 2 + 1:] = 0
+        self._ex, self._ex_key = None, None
+
+    def forward(self, x):
+        if self.mask_type != "A":
+            raise NotImplementedError("mask type B is not used by cheng2020 / mbt2018")
+        k = (self.weight.data_ptr(), self.weight._version, self.bias.data_ptr(), self.bias._version)
+        if self._ex is None or self._ex_key != k:
+            self._ex = EC.ChengContext({"weight": self.weight.detach(), "bias": self.bias.detach()}, prefix="")
+            self._ex_key = k
+        return K.from_nc4(self._ex.forward(K.to_nc4(x.detach().contiguous())), self.out_channels)
+
+
+# --------------------------------------------------------------------------- #
 # Entropy models (compressai.entropy_models; SURVEY Appendix A.3 / A.4)
 # --------------------------------------------------------------------------- #
 
@@ -353,7 +492,7 @@ class CompressionModel(nn.Module):
         key = tuple((p.data_ptr(), p._version) for p in self.parameters())
         if getattr(self, "_ck", None) is None or self._ck_key != key:
             sd = {k: v.detach() for k, v in self.state_dict().items()}
-            self._ck = E.CodecKernels(sd, self.model_kind)
+            self._ck = EC.ChengKernels(sd) if self.model_kind == "cheng2020" else E.CodecKernels(sd, self.model_kind)
             self._ck_key = key
         return self._ck
 
@@ -398,12 +537,39 @@ class ScaleHyperprior(CompressionModel):
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
 
 
+class Cheng2020Anchor(CompressionModel):
+    """compressai.models.Cheng2020Anchor (JointAutoregressiveHierarchicalPriors with residual transforms).
+    Eval-mode forward (the attack path); training this model is out of scope."""
+    model_kind = "cheng2020"
+
+    def __init__(self, N=192, **kwargs):
+        super().__init__()
+        M = N
+        self.entropy_bottleneck = EntropyBottleneck(N)
+        self.g_a = ChengAnalysisTransform(N)
+        self.h_a = ChengHyperAnalysis(N)
+        self.h_s = ChengHyperSynthesis(N)
+        self.g_s = ChengSynthesisTransform(N)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.context_prediction = MaskedConv2d(M, 2 * M, kernel_size=5, padding=2, stride=1)
+        self.entropy_parameters = EntropyParameters(M)
+        self.N, self.M = int(N), int(M)
+
+    def forward(self, x):
+        if self.training:
+            raise NotImplementedError("cheng2020 training is out of scope on the HIP path (eval forward only)")
+        res = self.kernels().forward(K.to_nc4(x.detach().contiguous()))
+        return {"x_hat": K.from_nc4(res["x_hat4"], 3),
+                "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
+
+
 # --------------------------------------------------------------------------- #
 # Zoo constructors (compressai.zoo; SURVEY Appendix A.1)
 # --------------------------------------------------------------------------- #
 _CFG = {
     "bmshj2018-factorized": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
     "bmshj2018-hyperprior": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
+    "cheng2020-anchor": {q: (128 if q <= 3 else 192, None) for q in range(1, 7)},
 }
 
 
@@ -432,3 +598,11 @@ def bmshj2018_hyperprior(quality, metric="mse", pretrained=False, progress=True,
     N, M = _CFG["bmshj2018-hyperprior"][quality]
     m = ScaleHyperprior(N, M)
     return _load_pretrained(m, "bmshj2018-hyperprior", quality, metric) if pretrained else m
+
+
+def cheng2020_anchor(quality, metric="mse", pretrained=False, progress=True, **kwargs):
+    if quality not in _CFG["cheng2020-anchor"]:
+        raise ValueError(f"cheng2020-anchor quality {quality} not in 1..6")
+    N, _ = _CFG["cheng2020-anchor"][quality]
+    m = Cheng2020Anchor(N)
+    return _load_pretrained(m, "cheng2020-anchor", quality, metric) if pretrained else m

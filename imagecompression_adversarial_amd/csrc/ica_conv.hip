@@ -29,7 +29,17 @@ enum {
   EPI_IGDN = 3,      // x = acc + bias; y = x * sqrt(beta' + gamma' x^2)
   EPI_GDN_BWD = 4,   // acc = dL/dy of a GDN; emit dL/dx  (needs saved y, s)
   EPI_IGDN_BWD = 5,  // same for IGDN
+  EPI_LRELU = 6,     // y = leaky_relu(acc + bias, 0.01)
+  EPI_LRELU_BWD = 7, // y = acc * (m > 0 ? 1 : 0.01), m = in_x (the saved leaky-ReLU output)
 };
+// Optional, runtime (uniform) extras of every epilogue:
+//   res      forward epilogues: y = act(...) + res (residual add after the activation);
+//            GDN_BWD/IGDN_BWD: acc += res before the GDN backward (gradient of out = gdn + skip)
+//   save_x   forward: the activation output before the residual add (GDN: y = x*s; LRELU: a);
+//            GDN_BWD/IGDN_BWD: the summed upstream gradient acc + res (feeds the skip branch)
+//   ps       (BIAS/RELU/LRELU) PixelShuffle(2) store: MFMA row rho = 16*c4 + 4*q + e is output
+//            channel 4*c4 + e at sub-pixel q = 2i + j of the (2 Hout) x (2 Wout) output
+//            (the host packs weights / bias in rho order)
 
 struct ConvParams {
   const float* x;     // input  nChw4c [N][ceil(Cin/4)][Hin][Win][4]
@@ -44,6 +54,10 @@ struct ConvParams {
   const float* in_s;  // bwd GDN: saved s
   int N, Cin, Hin, Win, Cout, Hout, Wout;
   float* save_t;      // bwd GDN (training): dL/dn per element, for the GDN parameter gradients
+  const float* res;   // optional residual (output layout), see above
+  const float* mask;  // conv_down fill_mode 1: leaky-ReLU mask source (input layout)
+  int fill_mode;      // conv_down: 0 plain, 1 x * lrelu'(mask), 2 PixelUnshuffle(2) view of x
+  int ps;             // PixelShuffle(2) store (BIAS/RELU/LRELU epilogues)
 };
 
 // --------------------------------------------------------------------------
@@ -60,7 +74,14 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
   const size_t pix = valid ? ((size_t)oy * p.Wout + ox) : 0;
   auto off = [&](int c4) -> size_t { return (((size_t)n * C4o + c4) * plane + pix) * 4; };
 
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU) {
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_LRELU) {
+    // PixelShuffle(2) store: output tensor [N][Cout/16][2 Hout][2 Wout][4]
+    const size_t plane2 = 4 * plane;
+    const size_t pix2 = valid ? ((size_t)(2 * oy) * (2 * p.Wout) + 2 * ox) : 0;
+    auto off_ps = [&](int c0) -> size_t {
+      const int c4 = c0 >> 4, q = (c0 >> 2) & 3;
+      return (((size_t)n * (p.Cout >> 4) + c4) * plane2 + pix2 + (size_t)(q >> 1) * (2 * p.Wout) + (q & 1)) * 4;
+    };
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
@@ -77,9 +98,37 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
             t = 0.f;
           }
           if constexpr (EPI == EPI_RELU) t = fmaxf(t, 0.f);
+          if constexpr (EPI == EPI_LRELU) t = t > 0.f ? t : t * 0.01f;
           v[e] = t;
         }
-        if (valid) st4(p.y + off(c0 >> 2), v);
+        if (valid) {
+          const size_t o = p.ps ? off_ps(c0) : off(c0 >> 2);
+          if (p.save_x) st4(p.save_x + o, v);
+          if (p.res) {
+            const f32x4 r = ld4(p.res + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += r[e];
+          }
+          st4(p.y + o, v);
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_LRELU_BWD) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c0 = co_base + it * 32 + 8 * g + 4 * h;
+        if (c0 >= p.Cout || !valid) continue;
+        const size_t o = off(c0 >> 2);
+        const f32x4 m = ld4(p.in_x + o);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = acc[it][4 * g + e];
+          v[e] = (c0 + e < p.Cout) ? (m[e] > 0.f ? t : t * 0.01f) : 0.f;
+        }
+        st4(p.y + o, v);
       }
     }
   } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
@@ -90,14 +139,6 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
-    if (p.save_x && valid) {
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          st4(p.save_x + off(it * 8 + 2 * g + h),
-              f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
-    }
 #pragma unroll
     for (int ct = 0; ct < IT; ++ct) {
       f32x16 nacc;
@@ -127,8 +168,14 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
             yv[e] = acc[ct][4 * g + e] * s;
           }
           const size_t o = off(ct * 8 + 2 * g + h);
-          st4(p.y + o, yv);
           if (p.save_s) st4(p.save_s + o, sv);
+          if (p.save_x) st4(p.save_x + o, yv);
+          if (p.res) {
+            const f32x4 r = ld4(p.res + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) yv[e] += r[e];
+          }
+          st4(p.y + o, yv);
         }
       }
     }
@@ -136,6 +183,38 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // acc = g = dL/dy.  t = (g x) dS/dn (GDN: -0.5 s^3, IGDN: 0.5/s) for all
     // channel tiles, then per output tile jt: u = gamma'^T t (16 live
     // accumulators) and dx = g s + 2 x u with x, s re-read (L2-hot).
+    // Residual gradient: added unconditionally (r = 0 without one) so that the accumulators are
+    // never live in two versions across a branch (that doubled the register footprint).
+    if (p.res || p.save_x) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const size_t o = off(it * 8 + 2 * g + h);
+          f32x4 r = {0.f, 0.f, 0.f, 0.f};
+          if (p.res && valid) r = ld4(p.res + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
+          if (p.save_x && valid)
+            st4(p.save_x + o, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+        }
+    }
+    // IT > 4 (C = 192): g*s is parked in the output (same-thread global write, re-read below) so that
+    // the 6 accumulator tiles are dead while the 6 t tiles and the u GEMM are live.
+    constexpr bool STASH = IT > 4;
+    if constexpr (STASH) {
+      if (valid) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const size_t o = off(it * 8 + 2 * g + h);
+            const f32x4 sv = ld4(p.in_s + o);
+            st4(p.y + o, f32x4{acc[it][4 * g] * sv[0], acc[it][4 * g + 1] * sv[1], acc[it][4 * g + 2] * sv[2],
+                               acc[it][4 * g + 3] * sv[3]});
+          }
+      }
+    }
     f32x16 tt[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it)
@@ -175,10 +254,16 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const size_t o = off(jt * 8 + 2 * g + h);
           const f32x4 xv = ld4(p.in_x + o), sv = ld4(p.in_s + o);
           f32x4 v;
+          if constexpr (STASH) {
+            const f32x4 gs = ld4(p.y + o);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            v[e] = acc[jt][r] * sv[e] + 2.0f * (xv[e] / sv[e]) * uacc[r];
+            for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * (xv[e] / sv[e]) * uacc[4 * g + e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g + e;
+              v[e] = acc[jt][r] * sv[e] + 2.0f * (xv[e] / sv[e]) * uacc[r];
+            }
           }
           st4(p.y + o, v);
         }
@@ -266,7 +351,21 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 #else
         if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
 #endif
-          v = ld4(p.x + ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4);
+          if (p.fill_mode == 2) {
+            // PixelUnshuffle(2): rho channel 16*c4g + 4*q + e of pixel (iy, ix) is channel 4*c4g + e
+            // of the (2 Hin) x (2 Win) tensor at sub-pixel q = 2i + j
+            const int c4g = c4 >> 2, q = c4 & 3;
+            v = ld4(p.x + ((((size_t)n * (Cin4 >> 2) + c4g) * (2 * p.Hin) + 2 * iy + (q >> 1)) * (2 * p.Win) +
+                           2 * ix + (q & 1)) * 4);
+          } else {
+            const size_t xo = ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4;
+            v = ld4(p.x + xo);
+            if (p.fill_mode == 1) {
+              const f32x4 m = ld4(p.mask + xo);
+#pragma unroll
+              for (int e2 = 0; e2 < 4; ++e2) v[e2] = m[e2] > 0.f ? v[e2] : v[e2] * 0.01f;
+            }
+          }
           if constexpr (CC == 4) {
 #pragma unroll
             for (int e2 = 0; e2 < 4; ++e2)
@@ -320,14 +419,20 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 // --------------------------------------------------------------------------
 constexpr int UP_TH = 4, UP_TW = 16, UP_PR = UP_TH + 2, UP_PC = UP_TW + 2, UP_PLANE = UP_PR * UP_PC;
 
-template <int PY, int PX, int IT, int EPI>
+// Generalised over the kernel size: ConvTranspose2d kKS s2 p(KS/2) op1, i.e. the input-gradient
+// of a stride-2 KSxKS conv with pad KS/2 (KS = 5: g_s deconvs / g_a dgrad; KS = 3, 1: the dgrad of
+// cheng2020's conv3x3 s2 and conv1x1 s2 skips).  Output y = 2a + PY uses taps
+// ky = ky0 + 2i, ky0 = (PY + PAD) & 1, at input row iy = a + (PY + PAD - ky) / 2 in [a-1, a+1].
+template <int KS, int PY, int PX, int IT, int EPI>
 ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
                            int nch) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int a_rel = jt * 2 + (j >> 4), b_rel = j & 15;
   constexpr int WSTEP = IT * 64 * 8;
-  constexpr int NY = (5 - PY + 1) / 2, NX = (5 - PX + 1) / 2;  // taps per axis (3 or 2)
-  const float* wl = p.wp + (size_t)cb * 25 * nch * WSTEP + (size_t)lane * 8;
+  constexpr int PAD = KS / 2;
+  constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
+  constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2;  // taps per axis
+  const float* wl = p.wp + (size_t)cb * KS * KS * nch * WSTEP + (size_t)lane * 8;
   f32x16 acc[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
@@ -336,14 +441,14 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
   const int total = NY * NX * nch;
   auto wptr = [&](int u) {
     const int ti = u / nch, ch = u - ti * nch;
-    const int ky = PY + 2 * (ti / NX), kx = PX + 2 * (ti % NX);
-    return wl + ((size_t)(ky * 5 + kx) * nch + ch) * WSTEP;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    return wl + ((size_t)(ky * KS + kx) * nch + ch) * WSTEP;
   };
   auto step = [&](float (&cur)[IT][8], float (&nxt)[IT][8], int u) {
     load_frag<IT, 8>(nxt, wptr(min(u + 1, total - 1)));  // unconditional: no phi copies
     const int ti = u / nch, ch = u - ti * nch;
-    const int ky = PY + 2 * (ti / NX), kx = PX + 2 * (ti % NX);
-    const int pr = a_rel + 1 + (PY + 2 - ky) / 2, pc = b_rel + 1 + (PX + 2 - kx) / 2;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
     const f32x4* pp = patch + (4 * ch + 2 * h) * UP_PLANE + pr * UP_PC + pc;
     const f32x4 v0 = pp[0], v1 = pp[UP_PLANE];
     const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
@@ -352,20 +457,22 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
 #pragma unroll
       for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
   };
-  float fa[IT][8], fb[IT][8];
-  load_frag<IT, 8>(fa, wptr(0));
-  int u = 0;
+  if constexpr (NY * NX > 0) {
+    float fa[IT][8], fb[IT][8];
+    load_frag<IT, 8>(fa, wptr(0));
+    int u = 0;
 #pragma unroll 1
-  for (; u + 1 < total; u += 2) {
-    step(fa, fb, u);
-    step(fb, fa, u + 1);
+    for (; u + 1 < total; u += 2) {
+      step(fa, fb, u);
+      step(fb, fa, u + 1);
+    }
+    if (u < total) step(fa, fb, u);
   }
-  if (u < total) step(fa, fb, u);
   const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
   conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
-template <int IT, int EPI>
+template <int KS, int IT, int EPI>
 __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   extern __shared__ f32x4 patch[];  // [Cin4][UP_PR][UP_PC]
   const int Hh = p.Hin, Wh = p.Win;
@@ -390,12 +497,13 @@ __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int jt = wave & 1, nch = p.Cin / 16;
+  // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
   if (wave < 2) {
-    conv_up_class<0, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
-    conv_up_class<1, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 0, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 1, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
   } else {
-    conv_up_class<0, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
-    conv_up_class<1, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 0, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 1, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
   }
 }
 
@@ -597,6 +705,27 @@ __global__ void pack_gdn_kernel(const float* __restrict__ gamma, const float* __
 // --------------------------------------------------------------------------
 // Host launchers (C ABI)
 // --------------------------------------------------------------------------
+// Instantiated (geometry, channel tile, epilogue) combinations; everything else returns -4/-5.
+//   (5,2): bmshj2018 g_a / g_s-dgrad / h_a     (3,1): all 3x3 s1 convs and their dgrads
+//   (3,2): cheng2020 strided 3x3               (1,2): cheng2020 strided 1x1 skips
+//   (1,1): entropy_parameters 1x1 stack         (5,1): MaskedConv2d context model
+template <int KS, int S, int IT, int EPI>
+constexpr bool down_variant() {
+  constexpr bool it_ok = IT == 1 || IT == 3 || IT == 4 || IT == 6;
+  constexpr bool gdn = EPI >= EPI_GDN && EPI <= EPI_IGDN_BWD;
+  if (!it_ok) return false;
+  if (KS == 5 && S == 2) return IT != 6 && (gdn ? IT == 4 : (EPI == EPI_BIAS || EPI == EPI_RELU));
+  if (KS == 3 && S == 1) return gdn ? (IT == 4 || IT == 6) : true;
+  if (KS == 3 && S == 2) return EPI == EPI_BIAS || EPI == EPI_LRELU;
+  if (KS == 1 && S == 2) return EPI == EPI_BIAS;
+  if (KS == 1 && S == 1) return EPI == EPI_BIAS || EPI == EPI_LRELU;
+  if (KS == 5 && S == 1) return EPI == EPI_BIAS;
+  return false;
+}
+// 4-channel chunks only where an RGB image is the conv input
+template <int KS, int S>
+constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) || (KS == 1 && S == 2); }
+
 template <int KS, int S, int IT, int CC, int TW, int EPI>
 static int launch_down(const ConvParams& p, hipStream_t st) {
   constexpr int TH = 128 / TW;
@@ -615,9 +744,18 @@ static int pick_tw_down(const ConvParams& p, hipStream_t st) {
 
 template <int KS, int S, int IT, int EPI>
 static int pick_cc_down(const ConvParams& p, hipStream_t st) {
-  if (p.Cin <= 4) return pick_tw_down<KS, S, IT, 4, EPI>(p, st);
-  if (p.Cin % 16 != 0) return -2;
-  return pick_tw_down<KS, S, IT, 16, EPI>(p, st);
+  if constexpr (!down_variant<KS, S, IT, EPI>()) {
+    return -4;
+  } else {
+    if (p.Cin <= 4) {
+      if constexpr (down_cc4<KS, S>()) return p.fill_mode ? -2 : pick_tw_down<KS, S, IT, 4, EPI>(p, st);
+      return -2;
+    }
+    // any Cin: the fill zeroes channel groups past Cin/4 and the packer zero-pads weight columns
+    // (nChw4c padding lanes are zero), so only the unshuffled view needs whole 16-channel chunks
+    if (p.fill_mode == 2 && p.Cin % 16 != 0) return -2;
+    return pick_tw_down<KS, S, IT, 16, EPI>(p, st);
+  }
 }
 
 template <int KS, int S, int EPI>
@@ -626,6 +764,7 @@ static int pick_it_down(const ConvParams& p, int it, hipStream_t st) {
     case 1: return pick_cc_down<KS, S, 1, EPI>(p, st);
     case 3: return pick_cc_down<KS, S, 3, EPI>(p, st);
     case 4: return pick_cc_down<KS, S, 4, EPI>(p, st);
+    case 6: return pick_cc_down<KS, S, 6, EPI>(p, st);
     default: return -3;
   }
 }
@@ -635,52 +774,100 @@ static int pick_epi_down(const ConvParams& p, int it, int epi, hipStream_t st) {
   switch (epi) {
     case EPI_BIAS: return pick_it_down<KS, S, EPI_BIAS>(p, it, st);
     case EPI_RELU: return pick_it_down<KS, S, EPI_RELU>(p, it, st);
-    case EPI_GDN: return it == 4 ? pick_cc_down<KS, S, 4, EPI_GDN>(p, st) : -4;
-    case EPI_IGDN: return it == 4 ? pick_cc_down<KS, S, 4, EPI_IGDN>(p, st) : -4;
-    case EPI_GDN_BWD: return it == 4 ? pick_cc_down<KS, S, 4, EPI_GDN_BWD>(p, st) : -4;
-    case EPI_IGDN_BWD: return it == 4 ? pick_cc_down<KS, S, 4, EPI_IGDN_BWD>(p, st) : -4;
+    case EPI_GDN: return pick_it_down<KS, S, EPI_GDN>(p, it, st);
+    case EPI_IGDN: return pick_it_down<KS, S, EPI_IGDN>(p, it, st);
+    case EPI_GDN_BWD: return pick_it_down<KS, S, EPI_GDN_BWD>(p, it, st);
+    case EPI_IGDN_BWD: return pick_it_down<KS, S, EPI_IGDN_BWD>(p, it, st);
+    case EPI_LRELU: return pick_it_down<KS, S, EPI_LRELU>(p, it, st);
+    case EPI_LRELU_BWD: return pick_it_down<KS, S, EPI_LRELU_BWD>(p, it, st);
     default: return -5;
   }
 }
 
-template <int IT, int EPI>
+static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, hipStream_t st) {
+  if (KS == 5 && S == 2) return pick_epi_down<5, 2>(p, it, epi, st);
+  if (KS == 3 && S == 1) return pick_epi_down<3, 1>(p, it, epi, st);
+  if (KS == 3 && S == 2) return pick_epi_down<3, 2>(p, it, epi, st);
+  if (KS == 1 && S == 2) return pick_epi_down<1, 2>(p, it, epi, st);
+  if (KS == 1 && S == 1) return pick_epi_down<1, 1>(p, it, epi, st);
+  if (KS == 5 && S == 1) return pick_epi_down<5, 1>(p, it, epi, st);
+  return -6;
+}
+
+template <int KS, int IT, int EPI>
 static int launch_up(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
   const size_t lds = (size_t)(p.Cin / 4) * UP_PLANE * sizeof(f32x4);
+  if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<IT, EPI>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<KS, IT, EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_kernel<IT, EPI>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL((conv_up_kernel<KS, IT, EPI>), grid, dim3(256), lds, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
-static int pick_up(const ConvParams& p, int it, int epi, hipStream_t st) {
-  if (it == 1) {
-    if (epi == EPI_BIAS) return launch_up<1, EPI_BIAS>(p, st);
-    if (epi == EPI_RELU) return launch_up<1, EPI_RELU>(p, st);
-    return -4;
-  }
-  if (it == 4) {
-    switch (epi) {
-      case EPI_BIAS: return launch_up<4, EPI_BIAS>(p, st);
-      case EPI_RELU: return launch_up<4, EPI_RELU>(p, st);
-      case EPI_GDN: return launch_up<4, EPI_GDN>(p, st);
-      case EPI_IGDN: return launch_up<4, EPI_IGDN>(p, st);
-      case EPI_GDN_BWD: return launch_up<4, EPI_GDN_BWD>(p, st);
-      case EPI_IGDN_BWD: return launch_up<4, EPI_IGDN_BWD>(p, st);
-      default: return -5;
+static int pick_up(const ConvParams& p, int KS, int it, int epi, hipStream_t st) {
+  if (p.fill_mode != 0 || p.ps != 0) return -4;
+  if (KS == 5) {
+    if (it == 1) {
+      if (epi == EPI_BIAS) return launch_up<5, 1, EPI_BIAS>(p, st);
+      if (epi == EPI_RELU) return launch_up<5, 1, EPI_RELU>(p, st);
+      return -4;
     }
+    if (it == 4) {
+      switch (epi) {
+        case EPI_BIAS: return launch_up<5, 4, EPI_BIAS>(p, st);
+        case EPI_RELU: return launch_up<5, 4, EPI_RELU>(p, st);
+        case EPI_GDN: return launch_up<5, 4, EPI_GDN>(p, st);
+        case EPI_IGDN: return launch_up<5, 4, EPI_IGDN>(p, st);
+        case EPI_GDN_BWD: return launch_up<5, 4, EPI_GDN_BWD>(p, st);
+        case EPI_IGDN_BWD: return launch_up<5, 4, EPI_IGDN_BWD>(p, st);
+        default: return -5;
+      }
+    }
+    return -3;
   }
-  return -3;
+  if (epi != EPI_BIAS) return -4;
+  if (KS == 3) {
+    if (it == 1) return launch_up<3, 1, EPI_BIAS>(p, st);
+    if (it == 4) return launch_up<3, 4, EPI_BIAS>(p, st);
+    if (it == 6) return launch_up<3, 6, EPI_BIAS>(p, st);
+    return -3;
+  }
+  if (KS == 1) {
+    if (it == 1) return launch_up<1, 1, EPI_BIAS>(p, st);
+    if (it == 4) return launch_up<1, 4, EPI_BIAS>(p, st);
+    if (it == 6) return launch_up<1, 6, EPI_BIAS>(p, st);
+    return -3;
+  }
+  return -6;
 }
 
+// C-ABI argument block of ica_conv_ex (mirrors include/ica_hip.h)
 extern "C" {
+typedef struct ica_conv_args {
+  const float* x;
+  float* y;
+  const float* wp;
+  const float* bias;
+  const float* gp;
+  const float* beta;
+  float* save_x;
+  float* save_s;
+  const float* in_x;
+  const float* in_s;
+  float* save_t;
+  const float* res;
+  const float* mask;
+  int N, Cin, Hin, Win, Cout, Hout, Wout;
+  int kind, KS, S, epi, it, fill_mode, ps;
+} ica_conv_args;
 
 // Channel tile (IT = number of 32-channel MFMA row tiles per wave) the conv
 // launchers use for a given output-channel count; the packer must agree.
@@ -691,17 +878,19 @@ int ica_conv_it(int cout) {
   return 4;
 }
 
-size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC) {
-  const int IT = ica_conv_it(O);
+static inline int resolve_it(int O, int it) { return it > 0 ? it : ica_conv_it(O); }
+
+size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC, int it) {
+  const int IT = resolve_it(O, it);
   const int ncb = (O + IT * 32 - 1) / (IT * 32);
   const int C4 = (C + 3) / 4, nch = (C4 * 4 + CC - 1) / CC;
   return (size_t)ncb * nch * KS * KS * IT * 64 * (CC / 2);
 }
 
 int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long so, long sc, int CC, int order,
-                         int flip, hipStream_t st) {
-  const int IT = ica_conv_it(O);
-  const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC);
+                         int flip, int it, hipStream_t st) {
+  const int IT = resolve_it(O, it);
+  const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC, IT);
   hipLaunchKernelGGL(pack_conv_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc, IT, CC,
                      order, total, flip);
   ICA_CHECK_LAUNCH();
@@ -747,10 +936,8 @@ int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, 
                   hipStream_t st) {
   ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout, save_t};
   const int it = ica_conv_it(Cout);
-  if (epi >= EPI_GDN && Cout != it * 32) return -4;
-  if (KS == 5 && S == 2) return pick_epi_down<5, 2>(p, it, epi, st);
-  if (KS == 3 && S == 1) return pick_epi_down<3, 1>(p, it, epi, st);
-  return -6;
+  if (epi >= EPI_GDN && epi <= EPI_IGDN_BWD && Cout != it * 32) return -4;
+  return pick_down(p, KS, S, it, epi, st);
 }
 
 int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
@@ -758,8 +945,23 @@ int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, in
                 float* save_s, const float* in_x, const float* in_s, float* save_t, hipStream_t st) {
   ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout, save_t};
   const int it = ica_conv_it(Cout);
-  if (epi >= EPI_GDN && Cout != it * 32) return -4;
-  return pick_up(p, it, epi, st);
+  if (epi >= EPI_GDN && epi <= EPI_IGDN_BWD && Cout != it * 32) return -4;
+  return pick_up(p, 5, it, epi, st);
+}
+
+int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
+  ConvParams p{a->x,    a->y,    a->wp,   a->bias, a->gp,   a->beta, a->save_x, a->save_s, a->in_x, a->in_s,
+               a->N,    a->Cin,  a->Hin,  a->Win,  a->Cout, a->Hout, a->Wout,   a->save_t, a->res,  a->mask,
+               a->fill_mode, a->ps};
+  const int it = resolve_it(a->Cout, a->it);
+  if (a->epi >= EPI_GDN && a->epi <= EPI_IGDN_BWD && a->Cout != it * 32) return -4;
+  if (a->ps && (a->Cout % 16 != 0 || !(a->epi == EPI_BIAS || a->epi == EPI_RELU || a->epi == EPI_LRELU))) return -4;
+  if (a->fill_mode == 1 && !a->mask) return -4;
+  if (a->fill_mode == 2 && a->Cin % 16 != 0) return -2;
+  if (a->epi == EPI_LRELU_BWD && !a->in_x) return -4;
+  if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, st);
+  if (a->kind == 1) return a->S == 2 ? pick_up(p, a->KS, it, a->epi, st) : -6;
+  return -6;
 }
 
 }  // extern "C"

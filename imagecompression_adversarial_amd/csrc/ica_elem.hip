@@ -399,6 +399,12 @@ __global__ void abs_kernel(const float* __restrict__ x, float* __restrict__ y, l
     y[i] = fabsf(x[i]);
 }
 
+// round half to even (torch.round / quantize "dequantize" with means=None; SURVEY §8 a16: rintf)
+__global__ void round_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = rintf(x[i]);
+}
+
 // per-image sum of squared differences (mse numerators) for nChw4c C4==1 tensors
 // or plain NCHW float tensors: both given as [B][len] with stride.
 __global__ void sqdiff_partial_kernel(const float* __restrict__ a, const float* __restrict__ b_,
@@ -548,6 +554,12 @@ int ica_pack_eb(const float* const* params, float* prm, float* med, int C, hipSt
   const float* const* p = params;
   hipLaunchKernelGGL(pack_eb_kernel, dim3((C + 63) / 64), dim3(64), 0, st, p[0], p[1], p[2], p[3], p[4], p[5], p[6],
                      p[7], p[8], p[9], p[10], p[11], p[12], p[13], p[14], prm, med, C);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_round(const float* x, float* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(round_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }

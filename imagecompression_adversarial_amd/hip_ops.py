@@ -10,9 +10,10 @@ import math
 
 import torch
 
-from ._lib import call, lib, ptr, stream
+from ._lib import ConvArgs, call, lib, ptr, stream
 
-EPI_BIAS, EPI_RELU, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD = range(6)
+EPI_BIAS, EPI_RELU, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD, EPI_LRELU, EPI_LRELU_BWD = range(8)
+FILL_PLAIN, FILL_LRELU_MASK, FILL_UNSHUFFLE = range(3)
 ORDER_DOWN, ORDER_UP = 0, 1
 GDN_BETA_BOUND = float((1e-6 + 2.0 ** -36) ** 0.5)  # NonNegativeParametrizer bound (utils/ops.py:67)
 
@@ -76,13 +77,14 @@ def from_nc4(x4: torch.Tensor, C: int) -> torch.Tensor:
 # Weight packing
 # --------------------------------------------------------------------------- #
 def pack_conv(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order: int, CC: int,
-              flip: bool = False) -> torch.Tensor:
-    """Pack a conv weight viewed as W[o][c][ky][kx] (strides so, sc; k contiguous); flip reverses the taps."""
+              flip: bool = False, it: int = 0) -> torch.Tensor:
+    """Pack a conv weight viewed as W[o][c][ky][kx] (strides so, sc; k contiguous); flip reverses the taps;
+    it = 32-channel row tiles per wave (0: the library default for O)."""
     w = w.detach().contiguous()
     _dev_check(w, "weight")
-    n = int(lib().ica_pack_conv_weight_size(O, Cc, KS, CC))
+    n = int(lib().ica_pack_conv_weight_size(O, Cc, KS, CC, it))
     dst = torch.empty(n, dtype=torch.float32, device=w.device)
-    call("ica_pack_conv_weight", ptr(w), ptr(dst), O, Cc, KS, so, sc, CC, order, int(flip), stream())
+    call("ica_pack_conv_weight", ptr(w), ptr(dst), O, Cc, KS, so, sc, CC, order, int(flip), it, stream())
     return dst
 
 
@@ -213,6 +215,45 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     return y, (y if ss is not None else None), ss
 
 
+def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: PackedGDN | None = None, res=None,
+            save_x=None, save_s=None, saved=None, save_t=None, mask=None, fill_mode=FILL_PLAIN, ps=False,
+            out=None, tag=None):
+    """Generic conv launch (ica_conv_ex).  kind 0: conv2d(x, W, stride S, pad KS//2); kind 1: the stride-2
+    transposed conv (dgrad of a stride-2 conv).  fill_mode 2 views x ([N, Cin/16, 2H, 2W, 4]) as the
+    PixelUnshuffle(2) tensor [N, Cin/4, H, W, 4] in rho order; ps stores PixelShuffle(2) of the rho-ordered
+    Cout rows (y: [N, Cout/16, 2Ho, 2Wo, 4]).  save_x / save_s / save_t: caller-allocated outputs."""
+    N, C4x, H, W, _ = x4.shape
+    if fill_mode == FILL_UNSHUFFLE:
+        if Cin != 16 * C4x:
+            raise RuntimeError("unshuffled conv input: Cin must be 16 * input channel groups")
+        H, W = H // 2, W // 2
+    if kind == 0:
+        Ho = (H + 2 * (KS // 2) - KS) // S + 1
+        Wo = (W + 2 * (KS // 2) - KS) // S + 1
+    else:
+        Ho, Wo = 2 * H, 2 * W
+    if out is not None:
+        y = out
+    elif ps:
+        y = torch.empty((N, Cout // 16, 2 * Ho, 2 * Wo, 4), dtype=torch.float32, device=x4.device)
+    else:
+        y = empty_nc4(N, Cout, Ho, Wo, x4.device)
+    in_x = in_s = None
+    if saved is not None:
+        in_x, in_s = saved
+    gp = None
+    if gdn is not None:
+        gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
+    a = ConvArgs(ptr(x4), ptr(y), ptr(wp), ptr(bias), ptr(gp), ptr(None if gdn is None else gdn.beta), ptr(save_x),
+                 ptr(save_s), ptr(in_x), ptr(in_s), ptr(save_t), ptr(res), ptr(mask), N, Cin, H, W, Cout, Ho, Wo,
+                 kind, KS, S, epi, it, fill_mode, int(bool(ps)))
+    import ctypes
+    ev = _ev_begin(tag)
+    call("ica_conv_ex", ctypes.c_void_p(ctypes.addressof(a)), stream())
+    _ev_end(ev)
+    return y
+
+
 # --------------------------------------------------------------------------- #
 # Reductions / elementwise
 # --------------------------------------------------------------------------- #
@@ -230,6 +271,12 @@ def reduce_rows(part: torch.Tensor, B: int, scale: float = 1.0, out=None):
 def abs_(x: torch.Tensor) -> torch.Tensor:
     y = torch.empty_like(x)
     call("ica_abs", ptr(x), ptr(y), x.numel(), stream())
+    return y
+
+
+def round_(x: torch.Tensor) -> torch.Tensor:
+    y = torch.empty_like(x)
+    call("ica_round", ptr(x), ptr(y), x.numel(), stream())
     return y
 
 

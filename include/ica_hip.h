@@ -42,12 +42,13 @@ enum { ICA_EPI_BIAS = 0, ICA_EPI_RELU = 1, ICA_EPI_GDN = 2, ICA_EPI_IGDN = 3, IC
 
 /* 32-channel MFMA row tiles per wave the launchers use for `cout` output channels. */
 int ica_conv_it(int cout);
-/* floats needed for the packed fragments of a weight viewed as W[O][C][KS][KS], chunk CC (4|16). */
-size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC);
+/* floats needed for the packed fragments of a weight viewed as W[O][C][KS][KS], chunk CC (4|16),
+ * it = 32-channel row tiles per wave (0: ica_conv_it(O)); conv launches must use the same it. */
+size_t ica_pack_conv_weight_size(int O, int C, int KS, int CC, int it);
 /* Pack W (element (o,c,ky,kx) at w[o*so + c*sc + ky*KS + kx]); order 0 = conv_down, 1 = conv_up.
  * flip != 0 reverses the taps (W[o][c][KS-1-ky][KS-1-kx]): the dgrad of a stride-1 conv as a conv_down. */
 int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long so, long sc, int CC, int order,
-                         int flip, hipStream_t stream);
+                         int flip, int it, hipStream_t stream);
 /* GDN reparametrisation + fragment packing: gamma' = max(gamma,2^-18)^2 - 2^-36 (transpose 0: gamma', 1: gamma'^T),
  * beta_eff = max(beta, beta_bound)^2 - 2^-36.  gp holds (C/32)^2 * 1024 floats. */
 int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_eff, int C, int transpose,
@@ -66,6 +67,35 @@ int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, 
 int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
                 int Cout, int Hout, int Wout, int epi, const float* gp, const float* beta, float* save_x,
                 float* save_s, const float* in_x, const float* in_s, float* save_t, hipStream_t stream);
+/* Generic launch (all geometries / epilogues / extras).  kind 0 = conv_down (stride-S KSxKS conv, pad KS/2;
+ * (KS,S) in {(5,2),(3,1),(3,2),(1,2),(1,1),(5,1)}), kind 1 = conv_up (stride-2 transposed conv, pad KS/2,
+ * output_padding 1; KS in {5,3,1} — the input-gradient of a stride-2 conv).  Epilogues add ICA_EPI_LRELU (6,
+ * slope 0.01) and ICA_EPI_LRELU_BWD (7: y = acc * (in_x > 0 ? 1 : 0.01)).  Optional extras:
+ *   res        forward: y = act(acc + bias) + res;  GDN_BWD/IGDN_BWD: acc += res first
+ *   save_x     forward: act output before the residual;  GDN_BWD/IGDN_BWD: acc + res
+ *   ps         PixelShuffle(2) store (rho-ordered rows: rho = 16*c4 + 4*q + e -> channel 4*c4+e, sub-pixel q)
+ *   fill_mode  conv_down input view: 1 = x * leaky_relu'(mask), 2 = PixelUnshuffle(2) of a (2H)x(2W) x
+ *   it         32-channel row tiles per wave (0 = ica_conv_it(Cout)); 6 runs C = 192 GDN layers in one wave.
+ * Reference: CompressAI cheng2020-anchor blocks (anchors/model.py:76-77). */
+enum { ICA_EPI_LRELU = 6, ICA_EPI_LRELU_BWD = 7 };
+typedef struct ica_conv_args {
+  const float* x;
+  float* y;
+  const float* wp;
+  const float* bias;
+  const float* gp;
+  const float* beta;
+  float* save_x;
+  float* save_s;
+  const float* in_x;
+  const float* in_s;
+  float* save_t;
+  const float* res;
+  const float* mask;
+  int N, Cin, Hin, Win, Cout, Hout, Wout;
+  int kind, KS, S, epi, it, fill_mode, ps;
+} ica_conv_args;
+int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);
 /* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
 size_t ica_pack_up3_size(int Cin);
 int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t stream);
@@ -98,6 +128,8 @@ int ica_eb_likelihood(const float* z, const float* prm, const float* med, const 
 /* params: host array of 15 device pointers (_matrix0..4, _bias0..4, _factor0..3, quantiles). */
 int ica_pack_eb(const float* const* params, float* prm, float* med, int C, hipStream_t stream);
 int ica_abs(const float* x, float* y, long n, hipStream_t stream);
+/* y = rint(x) (round half to even == torch.round): eval-mode quantize(y, "dequantize"), means = None. */
+int ica_round(const float* x, float* y, long n, hipStream_t stream);
 int ica_clamp01(const float* x, float* y, long n, hipStream_t stream);
 int ica_sqdiff_partial(const float* a, const float* b, float* part, int B, long len, int clamp_a, hipStream_t stream);
 int ica_nc4_bound_to_nchw(const float* x4, float* out, int B, int H, int W, int clamp, hipStream_t stream);

@@ -120,7 +120,7 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
                 raise ValueError(att_metric)
         if bool((~cheap).any()):
             idx = (~cheap).nonzero().flatten()
-            x_ = codec.g_s(P, codec.g_a(P, im_in[idx]))
+            x_ = codec.transforms(P, im_in[idx], model)
             out = codec.bound01(x_) if clamp else x_
             if att_metric == "L2":
                 if coupled:
@@ -157,7 +157,7 @@ def ifgsm(P, im_s, steps=10, epsilon=16.0, momentum=False, model="hyper"):
     g = torch.zeros_like(im_s)
     alpha = eps / steps
     for _ in range(steps):
-        out = codec.g_s(P, codec.g_a(P, im_adv))
+        out = codec.transforms(P, im_adv, model)
         d = output_s - out
         loss = _per_image_mean(d * d).sum()
         grad, = torch.autograd.grad(loss, im_adv)

@@ -13,6 +13,10 @@ Reference anchors:
   * EntropyBottleneck likelihood formula        utils/metrics_compare/decode.py:35-41 (text)
   * GaussianConditional likelihood               visual_distribution.py:85-101, attack_rd.py:46 (0.11 floor)
   * bpp                                          attack_rd.py:303,419
+  * cheng2020-anchor (CompressAI Cheng2020Anchor, built at anchors/model.py:76-77; composition
+    anchors/model.py:97-106): restated from the public CompressAI layer definitions (SURVEY §8 a17 and
+    Appendix A.7).  CompressAI is not vendored in /root/reference and not installed, so the
+    architecture itself is PARITY UNPINNED beyond its primitives (conv geometry, GDN, bounds).
 """
 from __future__ import annotations
 
@@ -240,6 +244,8 @@ def gaussian_conditional(y, scales, means=None, training=False, noise=None):
 # --------------------------------------------------------------------------- #
 def forward(P, x, model="hyper", training=False, noise_y=None, noise_z=None):
     """net(x) -> {"x_hat", "likelihoods": {"y", "z"}} (anchors/balle.py:25-55)."""
+    if model == "cheng2020":
+        return cheng_forward(P, x, training, noise_y, noise_z)
     y = g_a(P, x)
     if model == "factorized":
         y_hat, y_lik = entropy_bottleneck(P, y, training, noise_y)
@@ -251,6 +257,129 @@ def forward(P, x, model="hyper", training=False, noise_y=None, noise_z=None):
     scales = h_s(P, z_hat)
     y_hat, y_lik = gaussian_conditional(y, scales, None, training, noise_y)
     return {"x_hat": g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
+
+
+# --------------------------------------------------------------------------- #
+# cheng2020-anchor (CompressAI Cheng2020Anchor / JointAutoregressiveHierarchicalPriors)
+# --------------------------------------------------------------------------- #
+LRELU_SLOPE = 0.01  # nn.LeakyReLU() default
+
+
+def lrelu(x):
+    return F.leaky_relu(x, LRELU_SLOPE)
+
+
+def conv_k(x, w, b, stride=1):
+    """CompressAI conv3x3 / conv1x1: Conv2d(k, stride, padding=k//2)."""
+    return F.conv2d(x, w, b, stride=stride, padding=w.shape[-1] // 2)
+
+
+def subpel(x, w, b, r=2):
+    """subpel_conv3x3: Conv2d(in, out*r^2, 3, padding=1) -> PixelShuffle(r)."""
+    return F.pixel_shuffle(conv_k(x, w, b), r)
+
+
+def rb_stride(P, pre, x):
+    """ResidualBlockWithStride(stride=2): GDN(conv3x3(lrelu(conv3x3_s2(x)))) + conv1x1_s2(x)."""
+    out = lrelu(conv_k(x, P[f"{pre}.conv1.weight"], P[f"{pre}.conv1.bias"], 2))
+    out = conv_k(out, P[f"{pre}.conv2.weight"], P[f"{pre}.conv2.bias"])
+    out = gdn(out, P[f"{pre}.gdn.beta"], P[f"{pre}.gdn.gamma"])
+    return out + conv_k(x, P[f"{pre}.skip.weight"], P[f"{pre}.skip.bias"], 2)
+
+
+def rb(P, pre, x):
+    """ResidualBlock(N, N): lrelu(conv3x3(lrelu(conv3x3(x)))) + x."""
+    out = lrelu(conv_k(x, P[f"{pre}.conv1.weight"], P[f"{pre}.conv1.bias"]))
+    out = lrelu(conv_k(out, P[f"{pre}.conv2.weight"], P[f"{pre}.conv2.bias"]))
+    return out + x
+
+
+def rb_up(P, pre, x):
+    """ResidualBlockUpsample(2): IGDN(conv3x3(lrelu(subpel(x)))) + subpel_upsample(x)."""
+    out = lrelu(subpel(x, P[f"{pre}.subpel_conv.0.weight"], P[f"{pre}.subpel_conv.0.bias"]))
+    out = conv_k(out, P[f"{pre}.conv.weight"], P[f"{pre}.conv.bias"])
+    out = gdn(out, P[f"{pre}.igdn.beta"], P[f"{pre}.igdn.gamma"], inverse=True)
+    return out + subpel(x, P[f"{pre}.upsample.0.weight"], P[f"{pre}.upsample.0.bias"])
+
+
+def cheng_g_a(P, x):
+    x = rb_stride(P, "g_a.0", x)
+    x = rb(P, "g_a.1", x)
+    x = rb_stride(P, "g_a.2", x)
+    x = rb(P, "g_a.3", x)
+    x = rb_stride(P, "g_a.4", x)
+    x = rb(P, "g_a.5", x)
+    return conv_k(x, P["g_a.6.weight"], P["g_a.6.bias"], 2)
+
+
+def cheng_g_s(P, y):
+    y = rb(P, "g_s.0", y)
+    y = rb_up(P, "g_s.1", y)
+    y = rb(P, "g_s.2", y)
+    y = rb_up(P, "g_s.3", y)
+    y = rb(P, "g_s.4", y)
+    y = rb_up(P, "g_s.5", y)
+    y = rb(P, "g_s.6", y)
+    return subpel(y, P["g_s.7.0.weight"], P["g_s.7.0.bias"])
+
+
+def cheng_h_a(P, y):
+    z = lrelu(conv_k(y, P["h_a.0.weight"], P["h_a.0.bias"]))
+    z = lrelu(conv_k(z, P["h_a.2.weight"], P["h_a.2.bias"]))
+    z = lrelu(conv_k(z, P["h_a.4.weight"], P["h_a.4.bias"], 2))
+    z = lrelu(conv_k(z, P["h_a.6.weight"], P["h_a.6.bias"]))
+    return conv_k(z, P["h_a.8.weight"], P["h_a.8.bias"], 2)
+
+
+def cheng_h_s(P, z):
+    s = lrelu(conv_k(z, P["h_s.0.weight"], P["h_s.0.bias"]))
+    s = lrelu(subpel(s, P["h_s.2.0.weight"], P["h_s.2.0.bias"]))
+    s = lrelu(conv_k(s, P["h_s.4.weight"], P["h_s.4.bias"]))
+    s = lrelu(subpel(s, P["h_s.6.0.weight"], P["h_s.6.0.bias"]))
+    return conv_k(s, P["h_s.8.weight"], P["h_s.8.bias"])
+
+
+def context_mask(k=5):
+    """MaskedConv2d type 'A': zero the centre tap and everything after it in raster order."""
+    m = torch.ones(k, k)
+    m[k // 2, k // 2:] = 0
+    m[k // 2 + 1:] = 0
+    return m
+
+
+def context_prediction(P, y_hat):
+    w = P["context_prediction.weight"] * context_mask(P["context_prediction.weight"].shape[-1])
+    return F.conv2d(y_hat, w, P["context_prediction.bias"], padding=w.shape[-1] // 2)
+
+
+def entropy_parameters(P, t):
+    t = lrelu(conv_k(t, P["entropy_parameters.0.weight"], P["entropy_parameters.0.bias"]))
+    t = lrelu(conv_k(t, P["entropy_parameters.2.weight"], P["entropy_parameters.2.bias"]))
+    return conv_k(t, P["entropy_parameters.4.weight"], P["entropy_parameters.4.bias"])
+
+
+def cheng_forward(P, x, training=False, noise_y=None, noise_z=None):
+    """entropy_estimator for cheng2020 (anchors/model.py:97-106) + g_s(y_hat) (compressor :80-84)."""
+    y = cheng_g_a(P, x)
+    z = cheng_h_a(P, y)
+    z_hat, z_lik = entropy_bottleneck(P, z, training, noise_z)
+    params = cheng_h_s(P, z_hat)
+    if training:
+        y_hat = y + (noise_y if noise_y is not None else torch.empty_like(y).uniform_(-0.5, 0.5))
+    else:
+        y_hat = torch.round(y)   # quantize(y, "dequantize") with means=None
+    ctx = context_prediction(P, y_hat)
+    gp = entropy_parameters(P, torch.cat((params, ctx), dim=1))
+    scales, means = gp.chunk(2, 1)
+    _, y_lik = gaussian_conditional(y, scales, means, training, noise_y)
+    return {"x_hat": cheng_g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
+
+
+def transforms(P, x, model="hyper"):
+    """g_s(g_a(x)) without quantisation (the attack's expensive branch, attack_rd.py:344-349)."""
+    if model == "cheng2020":
+        return cheng_g_s(P, cheng_g_a(P, x))
+    return g_s(P, g_a(P, x))
 
 
 def bpp(likelihoods: dict, num_pixels: int):
@@ -285,6 +414,8 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
     def gd(name, C):
         P[f"{name}.beta"], P[f"{name}.gamma"] = gdn_init(C)
 
+    if model == "cheng2020":
+        return _init_cheng(P, cv, gd, gen, N)
     cv("g_a.0", N, 3, 5); gd("g_a.1", N)
     cv("g_a.2", N, N, 5); gd("g_a.3", N)
     cv("g_a.4", N, N, 5); gd("g_a.5", N)
@@ -301,6 +432,43 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
         cv("h_s.0", N, N, 5, True)
         cv("h_s.2", N, N, 5, True)
         cv("h_s.4", M, N, 3)
+    _init_eb(P, gen, eb_ch)
+    return P
+
+
+def _init_cheng(P, cv, gd, gen, N):
+    """Cheng2020Anchor(N) state-dict names / shapes (CompressAI), random init."""
+    for i in (0, 2, 4):   # ResidualBlockWithStride
+        cv(f"g_a.{i}.conv1", N, 3 if i == 0 else N, 3)
+        cv(f"g_a.{i}.conv2", N, N, 3)
+        gd(f"g_a.{i}.gdn", N)
+        cv(f"g_a.{i}.skip", N, 3 if i == 0 else N, 1)
+    for pre in ("g_a.1", "g_a.3", "g_a.5", "g_s.0", "g_s.2", "g_s.4", "g_s.6"):   # ResidualBlock
+        cv(f"{pre}.conv1", N, N, 3)
+        cv(f"{pre}.conv2", N, N, 3)
+    cv("g_a.6", N, N, 3)
+    for i in (1, 3, 5):   # ResidualBlockUpsample
+        cv(f"g_s.{i}.subpel_conv.0", 4 * N, N, 3)
+        cv(f"g_s.{i}.conv", N, N, 3)
+        gd(f"g_s.{i}.igdn", N)
+        cv(f"g_s.{i}.upsample.0", 4 * N, N, 3)
+    cv("g_s.7.0", 12, N, 3)
+    for i in (0, 2, 4, 6, 8):
+        cv(f"h_a.{i}", N, N, 3)
+    cv("h_s.0", N, N, 3)
+    cv("h_s.2.0", 4 * N, N, 3)
+    cv("h_s.4", N * 3 // 2, N, 3)
+    cv("h_s.6.0", 4 * (N * 3 // 2), N * 3 // 2, 3)
+    cv("h_s.8", 2 * N, N * 3 // 2, 3)
+    cv("context_prediction", 2 * N, N, 5)
+    cv("entropy_parameters.0", N * 10 // 3, N * 12 // 3, 1)
+    cv("entropy_parameters.2", N * 8 // 3, N * 10 // 3, 1)
+    cv("entropy_parameters.4", N * 6 // 3, N * 8 // 3, 1)
+    _init_eb(P, gen, N)
+    return P
+
+
+def _init_eb(P, gen, eb_ch):
     # EntropyBottleneck(C, filters=(3,3,3,3), init_scale=10) (A.3)
     filters = (1,) + EB_FILTERS + (1,)
     scale = 10.0 ** (1 / (len(EB_FILTERS) + 1))
@@ -311,7 +479,6 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
         if i < len(EB_FILTERS):
             P[f"entropy_bottleneck._factor{i}"] = torch.zeros((eb_ch, filters[i + 1], 1))
     P["entropy_bottleneck.quantiles"] = torch.tensor([-10.0, 0.0, 10.0]).repeat(eb_ch, 1, 1)
-    return P
 
 
 def perturb_params(P, seed=1, gdn_scale=0.3, eb_scale=0.5):
