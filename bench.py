@@ -1,4 +1,5 @@
-"""Benchmark: attack-step·images/s on Balle2018-hyperprior q3, 512x768 (BASELINE.json configs[1]).
+"""Benchmark: attack-step·images/s on Balle2018-hyperprior q3, 512x768 (BASELINE.json configs[1]);
+``--model cheng2020`` measures configs[2]'s per-GPU shard (cheng2020-anchor q6, 32 images of 768x512).
 
 One "step" = one attack_rd.attack_ iteration over the per-GPU batch: L-inf box
 + input clamp, g_a + g_s forward, loss, g_s + g_a input-gradient backward, Adam
@@ -49,26 +50,20 @@ def layer_flops(tag, N, M, H, W, B):
     return 2.0 * macs * B
 
 
-def step_flops(N, M, H, W, B):
-    tags = [f"{l}.{k}" for l in ("g_a.0", "g_a.2", "g_a.4", "g_a.6", "g_s.0", "g_s.2", "g_s.4", "g_s.6")
-            for k in ("fwd", "dgrad")]
-    return sum(layer_flops(t, N, M, H, W, B) for t in tags)
-
-
-def cpu_baseline(H, W, quality, seconds):
+def cpu_baseline(H, W, quality, seconds, model="hyper"):
     """The CPU oracle (PyTorch-CPU fp32 restatement, kind 'port') timed on this host:
     one reference attack step on ONE image, with weight gradients computed as the
     reference does (params require grad), bounded to ~`seconds` of CPU work."""
     from oracle import codec
     # the box's CPU share (OMP_NUM_THREADS is set to it there); never oversubscribe
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0)))))
-    P = codec.init_params("hyper", quality, seed=0)
+    P = codec.init_params(model, quality, seed=0)
     for v in P.values():
         v.requires_grad_(True)
     g = torch.Generator().manual_seed(0)
     im_s = torch.rand((1, 3, H, W), generator=g)
     with torch.no_grad():
-        os_ = torch.clamp(codec.g_s(P, torch.round(codec.g_a(P, im_s))), 0, 1)
+        os_ = torch.clamp(codec.forward(P, im_s, model)["x_hat"], 0, 1)
     noise = torch.zeros_like(im_s).requires_grad_(True)
     opt = torch.optim.Adam([noise], lr=0.01)
     eps = 16 / 255.0
@@ -77,7 +72,7 @@ def cpu_baseline(H, W, quality, seconds):
         nc = codec.bound01(noise, -eps, eps)
         im_in = codec.bound01(im_s + nc)
         li = torch.mean((im_s - im_in) ** 2)
-        o = codec.bound01(codec.g_s(P, codec.g_a(P, im_in)))
+        o = codec.bound01(codec.transforms(P, im_in, model))
         loss = 1.0 - torch.mean((os_ - o) ** 2) if li <= 1e-4 else li
         opt.zero_grad()
         loss.backward()
@@ -95,7 +90,7 @@ def cpu_baseline(H, W, quality, seconds):
     return {"value": n / el, "unit": "attack-step·images/s", "cores": torch.get_num_threads(),
             "kind": "port",
             "sample": f"oracle attack step (fwd+bwd incl. weight grads as the reference), 1 image {W}x{H}, "
-                      f"hyper q{quality}, {n} timed steps after 1 warm-up ({el:.1f} s)"}
+                      f"{model} q{quality}, {n} timed steps after 1 warm-up ({el:.1f} s)"}
 
 
 def main():
@@ -106,7 +101,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--width", type=int, default=768)
-    ap.add_argument("--quality", type=int, default=3)
+    ap.add_argument("--quality", type=int, default=None, help="default 3 (hyper) / 6 (cheng2020)")
+    ap.add_argument("--model", default="hyper", choices=("hyper", "cheng2020"))
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -125,11 +121,15 @@ def main():
     from imagecompression_adversarial_amd import hip_ops as K
     from imagecompression_adversarial_amd.attack import AttackLoop
     from imagecompression_adversarial_amd.engine import CodecKernels
+    from imagecompression_adversarial_amd.engine_cheng import ChengKernels
 
     H, W, B = args.height, args.width, args.batch
-    P = codec.init_params("hyper", args.quality, seed=0)
+    model = args.model
+    if args.quality is None:
+        args.quality = 6 if model == "cheng2020" else 3
+    P = codec.init_params(model, args.quality, seed=0)
     sd = {k: v.to(dev) for k, v in P.items()}
-    kern = CodecKernels(sd, "hyper")
+    kern = ChengKernels(sd) if model == "cheng2020" else CodecKernels(sd, "hyper")
     N, M = kern.N, kern.M
     gen = torch.Generator(device=dev).manual_seed(rank)
     im_s = torch.rand((B, 3, H, W), generator=gen, device=dev)
@@ -141,6 +141,7 @@ def main():
     if dist:
         dist.barrier()
     K.EVENT_HOOK = {}
+    K.FLOPS_HOOK = {}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
@@ -159,7 +160,11 @@ def main():
     per_tag = {tag: sum(a.elapsed_time(b) for a, b in evs) / len(evs) for tag, evs in hook.items()}
     dom = max(per_tag, key=lambda t: per_tag[t] * len(hook[t]))
     dom_ms = per_tag[dom]
-    dom_flops = layer_flops(dom, N, M, H, W, B)
+    if model == "cheng2020":   # per-launch algorithmic FLOPs recorded by hip_ops.conv_ex
+        flops_of = dict(K.FLOPS_HOOK)
+    else:
+        flops_of = {t: layer_flops(t, N, M, H, W, B) for t in per_tag}
+    dom_flops = flops_of[dom]
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     traffic = None
     tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -168,20 +173,24 @@ def main():
             traffic = json.load(open(tf)).get(dom)
         except Exception:
             traffic = None
-    total_flops = step_flops(N, M, H, W, B)
+    # network FLOPs of one step (every step of this loop takes the expensive branch: loss_i starts at 0)
+    total_flops = sum(flops_of[t] * len(hook[t]) for t in per_tag) / args.steps
     ms_step = el / args.steps * 1e3
     value = B * world * args.steps / el
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds)
+            cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds, model)
+        metric = METRIC if model == "hyper" else \
+            "attack-step·images/sec, Cheng2020-anchor q6 768×512 (configs[2] per-GPU shard)"
+        name = "hyper" if model == "hyper" else "cheng2020"
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world,
+            "metric": metric, "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (torch.rand images, seeded CompressAI-init weights)",
-            "config": {"workload": f"attack_rd -m hyper -q {args.quality} -att_metric L2 -noise 1e-4, "
+            "config": {"workload": f"attack_rd -m {name} -q {args.quality} -att_metric L2 -noise 1e-4, "
                                    f"{B} images/GPU of {W}x{H}, steps of the 1001-step loop",
                        "per_gpu_batch": B, "global_batch": B * world, "height": H, "width": W,
                        "parallelism": f"image-shard x{world} (no data-path collective)"},
@@ -189,6 +198,7 @@ def main():
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                          "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
+            "step_gflop_per_image": round(total_flops / B / 1e9, 2),
             "step_tflops": round(total_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
             "per_kernel_ms": {k: round(v, 4) for k, v in sorted(per_tag.items())},

@@ -32,7 +32,9 @@ enum {
   EPI_LRELU = 6,     // y = leaky_relu(acc + bias, 0.01)
   EPI_LRELU_BWD = 7, // y = acc * (m > 0 ? 1 : 0.01), m = in_x (the saved leaky-ReLU output)
 };
-// Optional, runtime (uniform) extras of every epilogue:
+// Compile-time feature flags (template parameter FX) so that plain layers compile to plain code:
+enum { FX_RES = 1, FX_PS = 2, FX_MASK = 4, FX_UNSHUF = 8, FX_T = 16 };  // FX_T: GDN-bwd writes save_t
+// Optional extras (present only in FX-enabled instantiations; res / save_x may still be null there):
 //   res      forward epilogues: y = act(...) + res (residual add after the activation);
 //            GDN_BWD/IGDN_BWD: acc += res before the GDN backward (gradient of out = gdn + skip)
 //   save_x   forward: the activation output before the residual add (GDN: y = x*s; LRELU: a);
@@ -65,7 +67,7 @@ struct ConvParams {
 // (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
 // float4 of channel group c4 = co_base/4 + it*8 + 2g + h.
 // --------------------------------------------------------------------------
-template <int IT, int EPI>
+template <int IT, int EPI, int FX>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
                            bool valid, int co_base) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -102,12 +104,16 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           v[e] = t;
         }
         if (valid) {
-          const size_t o = p.ps ? off_ps(c0) : off(c0 >> 2);
-          if (p.save_x) st4(p.save_x + o, v);
-          if (p.res) {
-            const f32x4 r = ld4(p.res + o);
+          size_t o;
+          if constexpr ((FX & FX_PS) != 0) o = off_ps(c0);
+          else o = off(c0 >> 2);
+          if constexpr ((FX & FX_RES) != 0) {
+            if (p.save_x) st4(p.save_x + o, v);
+            if (p.res) {
+              const f32x4 r = ld4(p.res + o);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += r[e];
+              for (int e = 0; e < 4; ++e) v[e] += r[e];
+            }
           }
           st4(p.y + o, v);
         }
@@ -169,11 +175,13 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           }
           const size_t o = off(ct * 8 + 2 * g + h);
           if (p.save_s) st4(p.save_s + o, sv);
-          if (p.save_x) st4(p.save_x + o, yv);
-          if (p.res) {
-            const f32x4 r = ld4(p.res + o);
+          if constexpr ((FX & FX_RES) != 0) {
+            if (p.save_x) st4(p.save_x + o, yv);
+            if (p.res) {
+              const f32x4 r = ld4(p.res + o);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) yv[e] += r[e];
+              for (int e = 0; e < 4; ++e) yv[e] += r[e];
+            }
           }
           st4(p.y + o, yv);
         }
@@ -185,7 +193,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // accumulators) and dx = g s + 2 x u with x, s re-read (L2-hot).
     // Residual gradient: added unconditionally (r = 0 without one) so that the accumulators are
     // never live in two versions across a branch (that doubled the register footprint).
-    if (p.res || p.save_x) {
+    if constexpr ((FX & FX_RES) != 0) {
 #pragma unroll
       for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -232,9 +240,11 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const float gx = acc[it][4 * g + e] * (xv[e] / s);  // in_x holds y = x*s: x = y / s
           tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
         }
-        if (p.save_t && valid)
-          st4(p.save_t + off(it * 8 + 2 * g + h),
-              f32x4{tt[it][4 * g], tt[it][4 * g + 1], tt[it][4 * g + 2], tt[it][4 * g + 3]});
+        if constexpr ((FX & FX_T) != 0) {
+          if (valid)
+            st4(p.save_t + off(it * 8 + 2 * g + h),
+                f32x4{tt[it][4 * g], tt[it][4 * g + 1], tt[it][4 * g + 2], tt[it][4 * g + 3]});
+        }
       }
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) {
@@ -305,7 +315,7 @@ ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
 // [cb][chunk][tap][it][lane][KH]  with  o = cb*IT*32 + it*32 + (lane&31),
 // c = chunk*CC + (lane>>5)*KH + s.
 // --------------------------------------------------------------------------
-template <int KS, int S, int IT, int CC, int TW, int EPI>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX>
 __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   constexpr int TH = 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
@@ -351,7 +361,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 #else
         if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
 #endif
-          if (p.fill_mode == 2) {
+          if constexpr ((FX & FX_UNSHUF) != 0) {
             // PixelUnshuffle(2): rho channel 16*c4g + 4*q + e of pixel (iy, ix) is channel 4*c4g + e
             // of the (2 Hin) x (2 Win) tensor at sub-pixel q = 2i + j
             const int c4g = c4 >> 2, q = c4 & 3;
@@ -360,7 +370,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
           } else {
             const size_t xo = ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4;
             v = ld4(p.x + xo);
-            if (p.fill_mode == 1) {
+            if constexpr ((FX & FX_MASK) != 0) {
               const f32x4 m = ld4(p.mask + xo);
 #pragma unroll
               for (int e2 = 0; e2 < 4; ++e2) v[e2] = m[e2] > 0.f ? v[e2] : v[e2] * 0.01f;
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   }
   if (g < total) step(fa, fb, g);
   const int oy = oy0 + oyl, ox = ox0 + oxl;
-  conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  conv_epilogue<IT, EPI, FX>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
 // --------------------------------------------------------------------------
@@ -423,7 +433,7 @@ constexpr int UP_TH = 4, UP_TW = 16, UP_PR = UP_TH + 2, UP_PC = UP_TW + 2, UP_PL
 // of a stride-2 KSxKS conv with pad KS/2 (KS = 5: g_s deconvs / g_a dgrad; KS = 3, 1: the dgrad of
 // cheng2020's conv3x3 s2 and conv1x1 s2 skips).  Output y = 2a + PY uses taps
 // ky = ky0 + 2i, ky0 = (PY + PAD) & 1, at input row iy = a + (PY + PAD - ky) / 2 in [a-1, a+1].
-template <int KS, int PY, int PX, int IT, int EPI>
+template <int KS, int PY, int PX, int IT, int EPI, int FX>
 ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
                            int nch) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
@@ -469,10 +479,10 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
     if (u < total) step(fa, fb, u);
   }
   const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
-  conv_epilogue<IT, EPI>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  conv_epilogue<IT, EPI, FX>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
-template <int KS, int IT, int EPI>
+template <int KS, int IT, int EPI, int FX>
 __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   extern __shared__ f32x4 patch[];  // [Cin4][UP_PR][UP_PC]
   const int Hh = p.Hin, Wh = p.Win;
@@ -499,11 +509,11 @@ __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   const int jt = wave & 1, nch = p.Cin / 16;
   // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
   if (wave < 2) {
-    conv_up_class<KS, 0, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
-    conv_up_class<KS, 1, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 0, 0, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 1, 1, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
   } else {
-    conv_up_class<KS, 0, 1, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
-    conv_up_class<KS, 1, 0, IT, EPI>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 0, 1, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 1, 0, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
   }
 }
 
@@ -705,12 +715,12 @@ __global__ void pack_gdn_kernel(const float* __restrict__ gamma, const float* __
 // --------------------------------------------------------------------------
 // Host launchers (C ABI)
 // --------------------------------------------------------------------------
-// Instantiated (geometry, channel tile, epilogue) combinations; everything else returns -4/-5.
+// Instantiated (geometry, channel tile, epilogue, features) combinations; others return -4/-5.
 //   (5,2): bmshj2018 g_a / g_s-dgrad / h_a     (3,1): all 3x3 s1 convs and their dgrads
 //   (3,2): cheng2020 strided 3x3               (1,2): cheng2020 strided 1x1 skips
 //   (1,1): entropy_parameters 1x1 stack         (5,1): MaskedConv2d context model
 template <int KS, int S, int IT, int EPI>
-constexpr bool down_variant() {
+constexpr bool down_base() {
   constexpr bool it_ok = IT == 1 || IT == 3 || IT == 4 || IT == 6;
   constexpr bool gdn = EPI >= EPI_GDN && EPI <= EPI_IGDN_BWD;
   if (!it_ok) return false;
@@ -722,79 +732,107 @@ constexpr bool down_variant() {
   if (KS == 5 && S == 1) return EPI == EPI_BIAS;
   return false;
 }
+template <int KS, int S, int IT, int EPI, int FX>
+constexpr bool down_variant() {
+  if (!down_base<KS, S, IT, EPI>()) return false;
+  if (FX == 0) return true;
+  if (FX == FX_T) return KS == 5 && S == 2 && (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD);  // bmshj2018 training
+  if (!(KS == 3 && S == 1)) return false;
+  switch (EPI) {
+    case EPI_BIAS: return FX == FX_RES || FX == FX_UNSHUF || FX == (FX_UNSHUF | FX_RES) || FX == FX_PS;
+    case EPI_LRELU: return FX == FX_RES || FX == FX_PS;
+    case EPI_LRELU_BWD: return FX == FX_MASK;
+    case EPI_GDN: case EPI_IGDN: case EPI_GDN_BWD: case EPI_IGDN_BWD: return FX == FX_RES;
+    default: return false;
+  }
+}
 // 4-channel chunks only where an RGB image is the conv input
 template <int KS, int S>
 constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) || (KS == 1 && S == 2); }
 
-template <int KS, int S, int IT, int CC, int TW, int EPI>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX>
 static int launch_down(const ConvParams& p, hipStream_t st) {
   constexpr int TH = 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
-template <int KS, int S, int IT, int CC, int EPI>
+template <int KS, int S, int IT, int CC, int EPI, int FX>
 static int pick_tw_down(const ConvParams& p, hipStream_t st) {
-  if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<KS, S, IT, CC, 32, EPI>(p, st);
-  return launch_down<KS, S, IT, CC, 16, EPI>(p, st);
+  if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<KS, S, IT, CC, 32, EPI, FX>(p, st);
+  return launch_down<KS, S, IT, CC, 16, EPI, FX>(p, st);
 }
 
-template <int KS, int S, int IT, int EPI>
+template <int KS, int S, int IT, int EPI, int FX>
 static int pick_cc_down(const ConvParams& p, hipStream_t st) {
-  if constexpr (!down_variant<KS, S, IT, EPI>()) {
+  if constexpr (!down_variant<KS, S, IT, EPI, FX>()) {
     return -4;
   } else {
     if (p.Cin <= 4) {
-      if constexpr (down_cc4<KS, S>()) return p.fill_mode ? -2 : pick_tw_down<KS, S, IT, 4, EPI>(p, st);
+      if constexpr (down_cc4<KS, S>() && (FX == 0 || FX == FX_T)) return pick_tw_down<KS, S, IT, 4, EPI, FX>(p, st);
       return -2;
     }
     // any Cin: the fill zeroes channel groups past Cin/4 and the packer zero-pads weight columns
     // (nChw4c padding lanes are zero), so only the unshuffled view needs whole 16-channel chunks
-    if (p.fill_mode == 2 && p.Cin % 16 != 0) return -2;
-    return pick_tw_down<KS, S, IT, 16, EPI>(p, st);
+    if ((FX & FX_UNSHUF) != 0 && p.Cin % 16 != 0) return -2;
+    return pick_tw_down<KS, S, IT, 16, EPI, FX>(p, st);
   }
 }
 
-template <int KS, int S, int EPI>
+template <int KS, int S, int EPI, int FX>
 static int pick_it_down(const ConvParams& p, int it, hipStream_t st) {
   switch (it) {
-    case 1: return pick_cc_down<KS, S, 1, EPI>(p, st);
-    case 3: return pick_cc_down<KS, S, 3, EPI>(p, st);
-    case 4: return pick_cc_down<KS, S, 4, EPI>(p, st);
-    case 6: return pick_cc_down<KS, S, 6, EPI>(p, st);
+    case 1: return pick_cc_down<KS, S, 1, EPI, FX>(p, st);
+    case 3: return pick_cc_down<KS, S, 3, EPI, FX>(p, st);
+    case 4: return pick_cc_down<KS, S, 4, EPI, FX>(p, st);
+    case 6: return pick_cc_down<KS, S, 6, EPI, FX>(p, st);
     default: return -3;
   }
 }
 
+template <int KS, int S, int EPI>
+static int pick_fx_down(const ConvParams& p, int it, int fx, hipStream_t st) {
+  switch (fx) {
+    case 0: return pick_it_down<KS, S, EPI, 0>(p, it, st);
+    case FX_RES: return pick_it_down<KS, S, EPI, FX_RES>(p, it, st);
+    case FX_PS: return pick_it_down<KS, S, EPI, FX_PS>(p, it, st);
+    case FX_MASK: return pick_it_down<KS, S, EPI, FX_MASK>(p, it, st);
+    case FX_UNSHUF: return pick_it_down<KS, S, EPI, FX_UNSHUF>(p, it, st);
+    case FX_UNSHUF | FX_RES: return pick_it_down<KS, S, EPI, FX_UNSHUF | FX_RES>(p, it, st);
+    case FX_T: return pick_it_down<KS, S, EPI, FX_T>(p, it, st);
+    default: return -4;
+  }
+}
+
 template <int KS, int S>
-static int pick_epi_down(const ConvParams& p, int it, int epi, hipStream_t st) {
+static int pick_epi_down(const ConvParams& p, int it, int epi, int fx, hipStream_t st) {
   switch (epi) {
-    case EPI_BIAS: return pick_it_down<KS, S, EPI_BIAS>(p, it, st);
-    case EPI_RELU: return pick_it_down<KS, S, EPI_RELU>(p, it, st);
-    case EPI_GDN: return pick_it_down<KS, S, EPI_GDN>(p, it, st);
-    case EPI_IGDN: return pick_it_down<KS, S, EPI_IGDN>(p, it, st);
-    case EPI_GDN_BWD: return pick_it_down<KS, S, EPI_GDN_BWD>(p, it, st);
-    case EPI_IGDN_BWD: return pick_it_down<KS, S, EPI_IGDN_BWD>(p, it, st);
-    case EPI_LRELU: return pick_it_down<KS, S, EPI_LRELU>(p, it, st);
-    case EPI_LRELU_BWD: return pick_it_down<KS, S, EPI_LRELU_BWD>(p, it, st);
+    case EPI_BIAS: return pick_fx_down<KS, S, EPI_BIAS>(p, it, fx, st);
+    case EPI_RELU: return pick_fx_down<KS, S, EPI_RELU>(p, it, fx, st);
+    case EPI_GDN: return pick_fx_down<KS, S, EPI_GDN>(p, it, fx, st);
+    case EPI_IGDN: return pick_fx_down<KS, S, EPI_IGDN>(p, it, fx, st);
+    case EPI_GDN_BWD: return pick_fx_down<KS, S, EPI_GDN_BWD>(p, it, fx, st);
+    case EPI_IGDN_BWD: return pick_fx_down<KS, S, EPI_IGDN_BWD>(p, it, fx, st);
+    case EPI_LRELU: return pick_fx_down<KS, S, EPI_LRELU>(p, it, fx, st);
+    case EPI_LRELU_BWD: return pick_fx_down<KS, S, EPI_LRELU_BWD>(p, it, fx, st);
     default: return -5;
   }
 }
 
-static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, hipStream_t st) {
-  if (KS == 5 && S == 2) return pick_epi_down<5, 2>(p, it, epi, st);
-  if (KS == 3 && S == 1) return pick_epi_down<3, 1>(p, it, epi, st);
-  if (KS == 3 && S == 2) return pick_epi_down<3, 2>(p, it, epi, st);
-  if (KS == 1 && S == 2) return pick_epi_down<1, 2>(p, it, epi, st);
-  if (KS == 1 && S == 1) return pick_epi_down<1, 1>(p, it, epi, st);
-  if (KS == 5 && S == 1) return pick_epi_down<5, 1>(p, it, epi, st);
+static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, int fx, hipStream_t st) {
+  if (KS == 5 && S == 2) return pick_epi_down<5, 2>(p, it, epi, fx, st);
+  if (KS == 3 && S == 1) return pick_epi_down<3, 1>(p, it, epi, fx, st);
+  if (KS == 3 && S == 2) return pick_epi_down<3, 2>(p, it, epi, fx, st);
+  if (KS == 1 && S == 2) return pick_epi_down<1, 2>(p, it, epi, fx, st);
+  if (KS == 1 && S == 1) return pick_epi_down<1, 1>(p, it, epi, fx, st);
+  if (KS == 5 && S == 1) return pick_epi_down<5, 1>(p, it, epi, fx, st);
   return -6;
 }
 
-template <int KS, int IT, int EPI>
+template <int KS, int IT, int EPI, int FX>
 static int launch_up(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
@@ -803,47 +841,58 @@ static int launch_up(const ConvParams& p, hipStream_t st) {
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<KS, IT, EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<KS, IT, EPI, FX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_kernel<KS, IT, EPI>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL((conv_up_kernel<KS, IT, EPI, FX>), grid, dim3(256), lds, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
-static int pick_up(const ConvParams& p, int KS, int it, int epi, hipStream_t st) {
-  if (p.fill_mode != 0 || p.ps != 0) return -4;
+static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStream_t st) {
   if (KS == 5) {
+    if (fx == FX_T && it == 4) {
+      if (epi == EPI_GDN_BWD) return launch_up<5, 4, EPI_GDN_BWD, FX_T>(p, st);
+      if (epi == EPI_IGDN_BWD) return launch_up<5, 4, EPI_IGDN_BWD, FX_T>(p, st);
+    }
+    if (fx != 0) return -4;
     if (it == 1) {
-      if (epi == EPI_BIAS) return launch_up<5, 1, EPI_BIAS>(p, st);
-      if (epi == EPI_RELU) return launch_up<5, 1, EPI_RELU>(p, st);
+      if (epi == EPI_BIAS) return launch_up<5, 1, EPI_BIAS, 0>(p, st);
+      if (epi == EPI_RELU) return launch_up<5, 1, EPI_RELU, 0>(p, st);
       return -4;
     }
     if (it == 4) {
       switch (epi) {
-        case EPI_BIAS: return launch_up<5, 4, EPI_BIAS>(p, st);
-        case EPI_RELU: return launch_up<5, 4, EPI_RELU>(p, st);
-        case EPI_GDN: return launch_up<5, 4, EPI_GDN>(p, st);
-        case EPI_IGDN: return launch_up<5, 4, EPI_IGDN>(p, st);
-        case EPI_GDN_BWD: return launch_up<5, 4, EPI_GDN_BWD>(p, st);
-        case EPI_IGDN_BWD: return launch_up<5, 4, EPI_IGDN_BWD>(p, st);
+        case EPI_BIAS: return launch_up<5, 4, EPI_BIAS, 0>(p, st);
+        case EPI_RELU: return launch_up<5, 4, EPI_RELU, 0>(p, st);
+        case EPI_GDN: return launch_up<5, 4, EPI_GDN, 0>(p, st);
+        case EPI_IGDN: return launch_up<5, 4, EPI_IGDN, 0>(p, st);
+        case EPI_GDN_BWD: return launch_up<5, 4, EPI_GDN_BWD, 0>(p, st);
+        case EPI_IGDN_BWD: return launch_up<5, 4, EPI_IGDN_BWD, 0>(p, st);
         default: return -5;
       }
     }
     return -3;
   }
-  if (epi != EPI_BIAS) return -4;
+  if (epi != EPI_BIAS || (fx & ~FX_RES) != 0) return -4;
   if (KS == 3) {
-    if (it == 1) return launch_up<3, 1, EPI_BIAS>(p, st);
-    if (it == 4) return launch_up<3, 4, EPI_BIAS>(p, st);
-    if (it == 6) return launch_up<3, 6, EPI_BIAS>(p, st);
+    if (fx == 0) {
+      if (it == 1) return launch_up<3, 1, EPI_BIAS, 0>(p, st);
+      if (it == 4) return launch_up<3, 4, EPI_BIAS, 0>(p, st);
+      if (it == 6) return launch_up<3, 6, EPI_BIAS, 0>(p, st);
+    } else {
+      if (it == 1) return launch_up<3, 1, EPI_BIAS, FX_RES>(p, st);
+      if (it == 4) return launch_up<3, 4, EPI_BIAS, FX_RES>(p, st);
+      if (it == 6) return launch_up<3, 6, EPI_BIAS, FX_RES>(p, st);
+    }
     return -3;
   }
   if (KS == 1) {
-    if (it == 1) return launch_up<1, 1, EPI_BIAS>(p, st);
-    if (it == 4) return launch_up<1, 4, EPI_BIAS>(p, st);
-    if (it == 6) return launch_up<1, 6, EPI_BIAS>(p, st);
+    if (fx != 0) return -4;
+    if (it == 1) return launch_up<1, 1, EPI_BIAS, 0>(p, st);
+    if (it == 4) return launch_up<1, 4, EPI_BIAS, 0>(p, st);
+    if (it == 6) return launch_up<1, 6, EPI_BIAS, 0>(p, st);
     return -3;
   }
   return -6;
@@ -937,7 +986,8 @@ int ica_conv_down(const float* x, float* y, const float* wp, const float* bias, 
   ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout, save_t};
   const int it = ica_conv_it(Cout);
   if (epi >= EPI_GDN && epi <= EPI_IGDN_BWD && Cout != it * 32) return -4;
-  return pick_down(p, KS, S, it, epi, st);
+  const int fx = (save_x ? FX_RES : 0) | (save_t ? FX_T : 0);
+  return pick_down(p, KS, S, it, epi, fx, st);
 }
 
 int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
@@ -946,7 +996,8 @@ int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, in
   ConvParams p{x, y, wp, bias, gp, beta, save_x, save_s, in_x, in_s, N, Cin, Hin, Win, Cout, Hout, Wout, save_t};
   const int it = ica_conv_it(Cout);
   if (epi >= EPI_GDN && epi <= EPI_IGDN_BWD && Cout != it * 32) return -4;
-  return pick_up(p, 5, it, epi, st);
+  const int fx = (save_x ? FX_RES : 0) | (save_t ? FX_T : 0);
+  return pick_up(p, 5, it, epi, fx, st);
 }
 
 int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
@@ -959,8 +1010,10 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   if (a->fill_mode == 1 && !a->mask) return -4;
   if (a->fill_mode == 2 && a->Cin % 16 != 0) return -2;
   if (a->epi == EPI_LRELU_BWD && !a->in_x) return -4;
-  if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, st);
-  if (a->kind == 1) return a->S == 2 ? pick_up(p, a->KS, it, a->epi, st) : -6;
+  const int fx = ((a->res || a->save_x) ? FX_RES : 0) | (a->ps ? FX_PS : 0) | (a->fill_mode == 1 ? FX_MASK : 0) |
+                 (a->fill_mode == 2 ? FX_UNSHUF : 0) | (a->save_t ? FX_T : 0);
+  if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, fx, st);
+  if (a->kind == 1) return a->S == 2 ? pick_up(p, a->KS, it, a->epi, fx, st) : -6;
   return -6;
 }
 

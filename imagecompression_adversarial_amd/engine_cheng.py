@@ -108,12 +108,13 @@ class Subpel:
                                                      flip=True, it=self.it_b)
 
     def forward(self, x4, epi=K.EPI_BIAS, **kw):
-        return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True, **kw)
+        return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,
+                         alg_rows=4 * self.C, **kw)
 
     def dgrad(self, g4, **kw):
         """g4: gradient of the shuffled output [N, C/4, 2H, 2W, 4] -> gradient of the input [N, Cin, H, W]."""
         return K.conv_ex(g4, self.R, self.bwd, None, self.Cin, 3, 1, 0, K.EPI_BIAS, self.it_b,
-                         fill_mode=K.FILL_UNSHUFFLE, **kw)
+                         fill_mode=K.FILL_UNSHUFFLE, alg_rows=4 * self.C, **kw)
 
 
 def _gdn(sd, pre):

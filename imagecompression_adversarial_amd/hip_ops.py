@@ -32,11 +32,18 @@ def _ev_begin(tag):
     return (tag, e0)
 
 
-def _ev_end(h):
+def _ev_end(h, flops=None):
     if h is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         EVENT_HOOK.setdefault(h[0], []).append((h[1], e1))
+        if flops is not None:
+            FLOPS_HOOK[h[0]] = flops
+
+
+# algorithmic FLOPs per tagged ica_conv_ex launch (filled while EVENT_HOOK is set): 2*MAC of the conv
+# (a transposed conv counts the MACs of the conv it differentiates) + the GDN channel GEMM if fused
+FLOPS_HOOK = {}
 
 
 def _dev_check(t: torch.Tensor, name="tensor"):
@@ -217,7 +224,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
 
 def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: PackedGDN | None = None, res=None,
             save_x=None, save_s=None, saved=None, save_t=None, mask=None, fill_mode=FILL_PLAIN, ps=False,
-            out=None, tag=None):
+            out=None, tag=None, alg_rows=None):
     """Generic conv launch (ica_conv_ex).  kind 0: conv2d(x, W, stride S, pad KS//2); kind 1: the stride-2
     transposed conv (dgrad of a stride-2 conv).  fill_mode 2 views x ([N, Cin/16, 2H, 2W, 4]) as the
     PixelUnshuffle(2) tensor [N, Cin/4, H, W, 4] in rho order; ps stores PixelShuffle(2) of the rho-ordered
@@ -250,7 +257,15 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
     import ctypes
     ev = _ev_begin(tag)
     call("ica_conv_ex", ctypes.c_void_p(ctypes.addressof(a)), stream())
-    _ev_end(ev)
+    if ev is not None:
+        px = N * (H * W if kind == 1 else Ho * Wo)
+        # alg_rows: real (non-padding) rows of a rho-ordered subpel weight (4 * C)
+        cin_alg = alg_rows if (fill_mode == FILL_UNSHUFFLE and alg_rows) else Cin
+        cout_alg = alg_rows if (ps and alg_rows) else Cout
+        fl = 2.0 * cin_alg * cout_alg * KS * KS * px
+        if epi in (EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD):
+            fl += 2.0 * Cout * Cout * N * Ho * Wo
+        _ev_end(ev, fl)
     return y
 
 
