@@ -15,6 +15,11 @@ loss_i are summed across ranks by one 4-byte-per-rank all-reduce per step
 (RCCL on the GPU box), and all gradients are normalised by the global image
 count, so N ranks reproduce one B_global run.
 
+``target=`` / ``roi=`` give the targeted / ROI attack (DESIGN.md "Targeted / ROI
+attack"): box-weighted masked means for the input budget and a minimised output loss that pulls the
+target region toward the codec's reconstruction of the target image and keeps the background at
+output_s.  Same step loop, schedule, branch rule and per-image semantics as above.
+
 ``ifgsm_batch`` == attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438) without
 random start (the reference default path), per image.
 """
@@ -60,6 +65,8 @@ class AttackResult:
     vi_msim: list = field(default_factory=list)
     noise: torch.Tensor | None = None
     branches: list = field(default_factory=list)
+    output_t: torch.Tensor | None = None   # targeted mode: clamp(x_hat(target))
+    tar_mse: torch.Tensor | None = None    # targeted mode: per-image mean_roi((out - output_t)^2)
 
 
 def eval_forward(kern: CodecKernels, x: torch.Tensor, clamp=True):
@@ -100,9 +107,12 @@ class AttackLoop:
     """Holds the device state of one batched attack_rd.attack_ run."""
 
     def __init__(self, kern: CodecKernels, im_s: torch.Tensor, steps=1001, epsilon=16.0, noise_thr=1e-4,
-                 lr=0.01, att_metric="L2", clamp=True, init_noise=None, coupled=False, group=None):
+                 lr=0.01, att_metric="L2", clamp=True, init_noise=None, coupled=False, group=None,
+                 target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0):
         if att_metric not in ("L2", "ms-ssim"):
             raise ValueError(f"att_metric {att_metric!r} not supported (reference: L2, ms-ssim)")
+        if target is not None and (att_metric != "L2" or coupled):
+            raise NotImplementedError("the targeted / ROI attack is defined for att_metric L2, per-image")
         self.kern = kern
         self.im_s = im_s.contiguous()
         B, C, H, W = im_s.shape
@@ -131,6 +141,15 @@ class AttackLoop:
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
         self.output_s, self.bpp_ori = eval_forward(kern, self.im_s, clamp)
         self.output_s4 = None
+        self.roi = None
+        if target is not None:
+            t = target.to(self.im_s.device).contiguous()
+            if t.shape[0] == 1 and B > 1:
+                t = t.expand(B, -1, -1, -1).contiguous()
+            if t.shape != self.im_s.shape:
+                raise ValueError(f"target {tuple(t.shape)} must match the source batch {tuple(self.im_s.shape)}")
+            self.output_t, _ = eval_forward(kern, t, True)   # attack_cv.py:136-137: the target's reconstruction
+            self.roi = roi_weights(H, W, roi, la_tar, la_bkg_in, la_bkg_out)
 
     def _adam_scalars(self, i):
         t = i + 1
@@ -146,7 +165,11 @@ class AttackLoop:
         y4, sa = kern.g_a(self.im_in4, save=True)
         xh4, ss = kern.g_s(y4, save=True)
         del y4
-        if self.metric == "L2":
+        if self.roi is not None:
+            x0, x1, y0, y1, _, _, wot, wob = self.roi
+            call("ica_roi_loss", ptr(xh4), ptr(self.output_s), ptr(self.output_t), ptr(self.grad4), ptr(self.part),
+                 B, H, W, x0, x1, y0, y1, wot, wob, int(self.clamp), stream())
+        elif self.metric == "L2":
             call("ica_attack_loss", ptr(xh4), ptr(self.output_s), ptr(self.grad4), ptr(self.part), B, H, W,
                  self.gscale, int(self.clamp), 0, stream())
         else:
@@ -162,6 +185,8 @@ class AttackLoop:
 
     def step(self, i, record_im_in=False, census=False):
         B, H, W = self.B, self.H, self.W
+        if self.roi is not None:
+            return self._step_roi(i, record_im_in, census)
         call("ica_attack_prologue", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
              self.eps, stream())
         K.reduce_rows(self.part, B, self.invN, out=self.loss_i)
@@ -183,6 +208,21 @@ class AttackLoop:
             return self.branch.tolist()
         return None
 
+    def _step_roi(self, i, record_im_in, census):
+        B, H, W = self.B, self.H, self.W
+        x0, x1, y0, y1, wit, wib, _, _ = self.roi
+        call("ica_roi_prologue", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
+             self.eps, x0, x1, y0, y1, wit, wib, stream())
+        K.reduce_rows(self.part, B, 1.0, out=self.loss_i)
+        gx4 = self.network_grad()
+        bc2s, neg_step = self._adam_scalars(i)
+        call("ica_roi_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(self.m), ptr(self.v),
+             ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr, bc2s, neg_step,
+             ptr(self.branch), x0, x1, y0, y1, wit, wib, stream())
+        if census:
+            return self.branch.tolist()
+        return None
+
     def run(self, record=False):
         branches = []
         for i in range(self.steps):
@@ -192,16 +232,42 @@ class AttackLoop:
         return branches
 
 
+def roi_weights(H, W, roi, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0):
+    """(x0, x1, y0, y1, w_in_tar, w_in_bkg, w_out_tar, w_out_bkg) of the masked means; roi = (x0, x1, y0, y1)
+    in pixels (x = width, attack_cv.py:159-161), None = the whole image is the target region."""
+    x0, x1, y0, y1 = (0, W, 0, H) if roi is None else (int(v) for v in roi)
+    x0, x1 = max(0, min(x0, W)), max(0, min(x1, W))
+    y0, y1 = max(0, min(y0, H)), max(0, min(y1, H))
+    area = max(x1 - x0, 0) * max(y1 - y0, 0)
+    if area == 0:
+        raise ValueError(f"empty ROI {roi} for a {W}x{H} image")
+    cnt_t, cnt_b = 3.0 * area, 3.0 * (H * W - area)
+    wb = (lambda la: float(la / cnt_b) if cnt_b > 0 else 0.0)
+    return (x0, x1, y0, y1, float(1.0 / cnt_t), wb(la_bkg_in), float(la_tar / cnt_t), wb(la_bkg_out))
+
+
+def roi_mse(a, b, roi4):
+    """Per-image mean over the target box of (a - b)^2 (NCHW)."""
+    x0, x1, y0, y1 = roi4
+    d = (a - b)[:, :, y0:y1, x0:x1]
+    return (d * d).flatten(1).mean(1)
+
+
 def attack_batch(kern: CodecKernels, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
                  clamp=True, init_noise=None, eval_msssim=True, record=False, coupled=False,
-                 group=None) -> AttackResult:
-    loop = AttackLoop(kern, im_s, steps, epsilon, noise_thr, lr, att_metric, clamp, init_noise, coupled, group)
+                 group=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0) -> AttackResult:
+    loop = AttackLoop(kern, im_s, steps, epsilon, noise_thr, lr, att_metric, clamp, init_noise, coupled, group,
+                      target, roi, la_tar, la_bkg_in, la_bkg_out)
     branches = loop.run(record=record)
     im_, out, bpp, mse_in, mse_out, msim_in, msim_out, vi, vi_msim = evaluate(
         kern, loop.im_in, loop.im_s, loop.output_s, clamp, adv=False, msssim=eval_msssim)
-    return AttackResult(im_adv=im_, output_adv=out, output_s=loop.output_s, bpp_ori=loop.bpp_ori, bpp=bpp,
-                        mse_in=mse_in, mse_out=mse_out, msim_in=msim_in, msim_out=msim_out, vi=vi, vi_msim=vi_msim,
-                        noise=loop.noise, branches=branches)
+    res = AttackResult(im_adv=im_, output_adv=out, output_s=loop.output_s, bpp_ori=loop.bpp_ori, bpp=bpp,
+                       mse_in=mse_in, mse_out=mse_out, msim_in=msim_in, msim_out=msim_out, vi=vi, vi_msim=vi_msim,
+                       noise=loop.noise, branches=branches)
+    if loop.roi is not None:
+        res.output_t = loop.output_t
+        res.tar_mse = roi_mse(out, loop.output_t, loop.roi[:4])
+    return res
 
 
 def ifgsm_batch(kern: CodecKernels, im_s, steps=10, epsilon=16.0, momentum=False, clamp=True):

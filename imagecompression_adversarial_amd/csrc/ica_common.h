@@ -44,3 +44,16 @@ ICA_DEV float wave_sum(float v) {
     hipError_t _e = hipGetLastError();              \
     if (_e != hipSuccess) return (int)_e;           \
   } while (0)
+
+// Targeted / ROI attack weights: box [y0, y1) x [x0, x1) is the target region.
+// Per-element loss weights: input term  w_in  = tar ? 1/cnt_tar : la_bkg_in/cnt_bkg,
+//                           output term w_out = tar ? la_tar/cnt_tar : la_bkg_out/cnt_bkg
+// (cnt = 3 * pixels of the region; a zero count gives weight 0).
+struct RoiBox {
+  int x0, x1, y0, y1;
+  float w_in_tar, w_in_bkg, w_out_tar, w_out_bkg;
+};
+ICA_DEV bool roi_inside(const RoiBox& r, long pix, long W) {
+  const long y = pix / W, x = pix - y * W;
+  return x >= r.x0 && x < r.x1 && y >= r.y0 && y < r.y1;
+}

@@ -148,16 +148,89 @@ __global__ void attack_loss_kernel(const float* __restrict__ xhat4, const float*
   if (threadIdx.x == 0) part[(long)b * gridDim.x + blockIdx.x] = r;
 }
 
+// Targeted / ROI attack (semantics in DESIGN.md "Targeted / ROI attack"):
+//   loss_i = mean_tar((s - ii)^2) + la_bkg_in * mean_bkg((s - ii)^2)              (box-weighted, per image)
+//   loss_o = la_tar * mean_tar((ot - o)^2) + la_bkg_out * mean_bkg((os - o)^2)     (minimised)
+// with o = Up(Low(x_hat, 0), 1) when clamping; ot = the codec's reconstruction of the target image.
+__global__ void roi_prologue_kernel(const float* __restrict__ noise, const float* __restrict__ im_s,
+                                    float* __restrict__ im_in4, float* __restrict__ part, long HW, long W, float eps,
+                                    RoiBox roi) {
+  __shared__ float sh[4];
+  const int b = blockIdx.y;
+  const float* nz = noise + (long)b * 3 * HW;
+  const float* is = im_s + (long)b * 3 * HW;
+  float* o4 = im_in4 + (long)b * 4 * HW;
+  float acc = 0.f;
+  for (long pix = (long)blockIdx.x * 256 + threadIdx.x; pix < HW; pix += (long)gridDim.x * 256) {
+    const float w = roi_inside(roi, pix, W) ? roi.w_in_tar : roi.w_in_bkg;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float nc = fminf(fmaxf(nz[c * HW + pix], -eps), eps);
+      const float s = is[c * HW + pix];
+      const float u = fadd_rn(s, nc);
+      const float ii = fminf(fmaxf(u, 0.f), 1.f);
+      v[c] = ii;
+      const float d = fsub_rn(s, ii);
+      acc = fadd_rn(acc, fmul_rn(w, fmul_rn(d, d)));
+    }
+    st4(o4 + pix * 4, v);
+  }
+  const float r = block_sum_256(acc, sh);
+  if (threadIdx.x == 0) part[(long)b * gridDim.x + blockIdx.x] = r;
+}
+
+__global__ void roi_loss_kernel(const float* __restrict__ xhat4, const float* __restrict__ out_s,
+                                const float* __restrict__ out_t, float* __restrict__ grad4, float* __restrict__ part,
+                                long HW, long W, RoiBox roi, int clamp) {
+  __shared__ float sh[4];
+  const int b = blockIdx.y;
+  const float* x4 = xhat4 + (long)b * 4 * HW;
+  const float* os = out_s + (long)b * 3 * HW;
+  const float* ot = out_t + (long)b * 3 * HW;
+  float* g4 = grad4 + (long)b * 4 * HW;
+  float acc = 0.f;
+  for (long pix = (long)blockIdx.x * 256 + threadIdx.x; pix < HW; pix += (long)gridDim.x * 256) {
+    const bool tar = roi_inside(roi, pix, W);
+    const float w = tar ? roi.w_out_tar : roi.w_out_bkg;
+    const float* ref = tar ? ot : os;
+    const f32x4 xv = ld4(x4 + pix * 4);
+    f32x4 gv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float xh = xv[c];
+      const float lo = fmaxf(xh, 0.f);
+      const float o = clamp ? fminf(lo, 1.f) : xh;
+      const float d = fsub_rn(ref[c * HW + pix], o);
+      acc = fadd_rn(acc, fmul_rn(w, fmul_rn(d, d)));
+      const float t = fmul_rn(w, d);
+      float g = -fadd_rn(t, t);
+      if (clamp) {
+        g = (lo <= 1.f || g > 0.f) ? g : g * 0.f;  // Up_bound backward
+        g = (xh >= 0.f || g < 0.f) ? g : g * 0.f;  // Low_bound backward
+      }
+      gv[c] = g;
+    }
+    st4(g4 + pix * 4, gv);
+  }
+  const float r = block_sum_256(acc, sh);
+  if (threadIdx.x == 0) part[(long)b * gridDim.x + blockIdx.x] = r;
+}
+
 // Branch select + bounds backward + torch Adam step on the noise (in place).
 //   cheap[b] = loss_i[b] > thr  -> g = -2*fl(invN*(im_s - im_in))   (L2 input loss)
 //   else                        -> g = g_net (nChw4c)               (network gradient)
 // Adam (torch 2.x op order): m = fma(1-b1, g-m, m); v = v*b2 + ((1-b2)*g)*g;
 // denom = sqrt(v)/bc2s + eps; p = p + neg_step*(m/denom)
+// ROI (targeted / masked attack): the cheap-branch input loss is the box-weighted mean, so the
+// per-element weight w_in(pixel) replaces invN (same op order: t = w*(s - ii), g = -(t + t)).
+template <bool ROI>
 __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __restrict__ im_s,
                                    const float* __restrict__ gnet4, const float* __restrict__ loss_i,
                                    const float* __restrict__ cheap_grad, float* __restrict__ m,
                                    float* __restrict__ v, float* __restrict__ im_in_out, long HW, float eps,
-                                   float thr, float invN, float bc2s, float neg_step, int* __restrict__ branch) {
+                                   float thr, float invN, float bc2s, float neg_step, int* __restrict__ branch,
+                                   RoiBox roi, long W) {
   const int b = blockIdx.y;
   const bool cheap = loss_i[b] > thr;
   if (branch && blockIdx.x == 0 && threadIdx.x == 0) branch[b] = cheap ? 1 : 0;
@@ -180,7 +253,9 @@ __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __res
         if (cheap_grad) {
           g = cheap_grad[i];
         } else {
-          const float t = fmul_rn(invN, fsub_rn(s, ii));
+          float w = invN;
+          if constexpr (ROI) w = roi_inside(roi, pix, W) ? roi.w_in_tar : roi.w_in_bkg;
+          const float t = fmul_rn(w, fsub_rn(s, ii));
           g = -fadd_rn(t, t);
         }
       } else {
@@ -510,8 +585,38 @@ int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float*
 int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
                     float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
                     float bc2s, float neg_step, int* branch, hipStream_t st) {
-  hipLaunchKernelGGL(attack_adam_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
-                     loss_i, cheap_grad, m, v, im_in_out, (long)H * W, eps, thr, invN, bc2s, neg_step, branch);
+  hipLaunchKernelGGL(attack_adam_kernel<false>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
+                     loss_i, cheap_grad, m, v, im_in_out, (long)H * W, eps, thr, invN, bc2s, neg_step, branch,
+                     RoiBox{}, (long)W);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_roi_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W, float eps,
+                     int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t st) {
+  const RoiBox roi{x0, x1, y0, y1, w_in_tar, w_in_bkg, 0.f, 0.f};
+  hipLaunchKernelGGL(roi_prologue_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, im_in4, part,
+                     (long)H * W, (long)W, eps, roi);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_roi_loss(const float* xhat4, const float* out_s, const float* out_t, float* grad4, float* part, int B, int H,
+                 int W, int x0, int x1, int y0, int y1, float w_out_tar, float w_out_bkg, int clamp, hipStream_t st) {
+  const RoiBox roi{x0, x1, y0, y1, 0.f, 0.f, w_out_tar, w_out_bkg};
+  hipLaunchKernelGGL(roi_loss_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, xhat4, out_s, out_t, grad4,
+                     part, (long)H * W, (long)W, roi, clamp);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, float* m, float* v,
+                 float* im_in_out, int B, int H, int W, float eps, float thr, float bc2s, float neg_step, int* branch,
+                 int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t st) {
+  const RoiBox roi{x0, x1, y0, y1, w_in_tar, w_in_bkg, 0.f, 0.f};
+  hipLaunchKernelGGL(attack_adam_kernel<true>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
+                     loss_i, nullptr, m, v, im_in_out, (long)H * W, eps, thr, 0.f, bc2s, neg_step, branch, roi,
+                     (long)W);
   ICA_CHECK_LAUNCH();
   return 0;
 }

@@ -118,6 +118,19 @@ int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float*
 int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
                     float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
                     float bc2s, float neg_step, int* branch, hipStream_t stream);
+/* Targeted / ROI attack (SURVEY §8f rank 1; README "attack with ROI", attack_cv.py:153-163 mask box,
+ * attack_data.py:202-226 target / masked losses; semantics fixed in DESIGN.md).  Box [y0,y1) x [x0,x1) is the
+ * target region; w_* are the per-element weights of the masked means (1/count, la_*/count).
+ * prologue: im_in4 as ica_attack_prologue, part = box-weighted input distortion (loss_i after ica_reduce_rows).
+ * loss: grad4 = d/dx_hat [w_out_tar * sum_tar (out_t - o)^2 + w_out_bkg * sum_bkg (out_s - o)^2], o = bound01(x_hat).
+ * adam: ica_attack_adam with the box-weighted cheap-branch gradient. */
+int ica_roi_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W, float eps,
+                     int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t stream);
+int ica_roi_loss(const float* xhat4, const float* out_s, const float* out_t, float* grad4, float* part, int B, int H,
+                 int W, int x0, int x1, int y0, int y1, float w_out_tar, float w_out_bkg, int clamp, hipStream_t stream);
+int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, float* m, float* v,
+                 float* im_in_out, int B, int H, int W, float eps, float thr, float bc2s, float neg_step, int* branch,
+                 int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t stream);
 int ica_ifgsm_step(float* x, const float* im_s, const float* grad4, float* gacc, const float* l1, int B, int H, int W,
                    float alpha, float eps, int momentum, hipStream_t stream);
 int ica_l1_partial(const float* g4, float* part, int B, int H, int W, hipStream_t stream);

@@ -73,12 +73,32 @@ def eval_batch(P, im_adv, im_s, output_s, model="hyper", clamp=True, adv=False, 
                            msim_in=msim_in, msim_out=msim_out, vi=vi, vi_msim=vi_msim)
 
 
+def _roi_masks(H, W, roi):
+    x0, x1, y0, y1 = (0, W, 0, H) if roi is None else roi
+    m = torch.zeros(1, 1, H, W)
+    m[:, :, y0:y1, x0:x1] = 1.0     # attack_cv.py:159-161 (x = width, y = height)
+    return m, 1.0 - m
+
+
+def _masked_mean(e, m):
+    """Per-image mean of e over the elements where m == 1 (3 channels each); 0 for an empty region."""
+    cnt = 3.0 * m.sum()
+    if float(cnt) == 0.0:
+        return torch.zeros(e.shape[0], dtype=e.dtype)
+    return (e * m).flatten(1).sum(1) / cnt
+
+
 def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
            clamp=True, model="hyper", coupled=False, init_noise=None, eval_msssim=True,
-           record=None):
+           record=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0):
     """attack_rd.attack_ restated (Adam on additive noise, L-inf box in the forward).
 
     record: optional list; per step appends dict(loss_i, branch) for trajectory tests.
+    target / roi: the targeted / ROI attack (SURVEY §8f rank 1, semantics as DESIGN.md states them;
+    the reference's own masked loss (attack_data.py:219-221) multiplies scalar means by mask tensors, so
+    its masked means are restated here as proper per-region means):
+      loss_i = mean_tar((s - ii)^2) + la_bkg_in * mean_bkg((s - ii)^2)
+      loss_o = la_tar * mean_tar((out_t - o)^2) + la_bkg_out * mean_bkg((out_s - o)^2)   (minimised)
     """
     B = im_s.shape[0]
     with torch.no_grad():
@@ -88,6 +108,9 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
         bpp_ori = torch.stack([codec.bpp({k: v[b:b + 1] for k, v in res["likelihoods"].items()}, H * W)
                                for b in range(B)])
     noise_range = epsilon / 255.0
+    if target is not None:
+        return _attack_roi(P, im_s, output_s, bpp_ori, steps, noise_range, noise_thr, lr, clamp, model,
+                           init_noise, eval_msssim, record, target, roi, la_tar, la_bkg_in, la_bkg_out)
     noise = torch.zeros_like(im_s) if init_noise is None else init_noise.clone()
     noise.requires_grad_(True)
     opt = torch.optim.Adam([noise], lr=lr)
@@ -145,6 +168,50 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
     ev = eval_batch(P, im_in, im_s, output_s, model, clamp, adv=False, msssim=eval_msssim)
     return SimpleNamespace(im_adv=ev.im, output_adv=ev.out, output_s=output_s, bpp_ori=bpp_ori,
                            bpp=ev.bpp, eval=ev, noise=noise.detach(), im_in=im_in)
+
+
+def _attack_roi(P, im_s, output_s, bpp_ori, steps, noise_range, noise_thr, lr, clamp, model, init_noise,
+                eval_msssim, record, target, roi, la_tar, la_bkg_in, la_bkg_out):
+    B, _, H, W = im_s.shape
+    with torch.no_grad():
+        t = target.expand_as(im_s) if target.shape[0] == 1 else target
+        output_t = torch.clamp(codec.forward(P, t, model)["x_hat"], 0.0, 1.0)
+    m_tar, m_bkg = _roi_masks(H, W, roi)
+    noise = torch.zeros_like(im_s) if init_noise is None else init_noise.clone()
+    noise.requires_grad_(True)
+    opt = torch.optim.Adam([noise], lr=lr)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1, 2, 3], gamma=0.33)
+    im_in = None
+    for i in range(steps):
+        noise_c = codec.UpBound.apply(codec.LowBound.apply(noise, -noise_range), noise_range)
+        im_in = codec.UpBound.apply(codec.LowBound.apply(im_s + noise_c, 0.0), 1.0)
+        d_in = (im_s - im_in) ** 2
+        li_b = _masked_mean(d_in, m_tar) + la_bkg_in * _masked_mean(d_in, m_bkg)
+        cheap = li_b > noise_thr
+        losses = torch.zeros((), dtype=im_s.dtype)
+        if bool(cheap.any()):
+            losses = losses + li_b[cheap].sum()
+        if bool((~cheap).any()):
+            idx = (~cheap).nonzero().flatten()
+            x_ = codec.transforms(P, im_in[idx], model)
+            out = codec.bound01(x_) if clamp else x_
+            lo = la_tar * _masked_mean((output_t[idx] - out) ** 2, m_tar) + \
+                la_bkg_out * _masked_mean((output_s[idx] - out) ** 2, m_bkg)
+            losses = losses + lo.sum()
+        if record is not None:
+            record.append({"loss_i": li_b.detach().clone(), "cheap": cheap.clone(), "lr": opt.param_groups[0]["lr"]})
+        opt.zero_grad()
+        losses.backward()
+        opt.step()
+        if i % max(steps // 3, 1) == 0:
+            sch.step()
+    im_in = im_in.detach()
+    ev = eval_batch(P, im_in, im_s, output_s, model, clamp, adv=False, msssim=eval_msssim)
+    x0, x1, y0, y1 = (0, W, 0, H) if roi is None else roi
+    dd = (ev.out - output_t)[:, :, y0:y1, x0:x1]
+    tar_mse = (dd * dd).flatten(1).mean(1)
+    return SimpleNamespace(im_adv=ev.im, output_adv=ev.out, output_s=output_s, bpp_ori=bpp_ori, bpp=ev.bpp, eval=ev,
+                           noise=noise.detach(), im_in=im_in, output_t=output_t, tar_mse=tar_mse)
 
 
 def ifgsm(P, im_s, steps=10, epsilon=16.0, momentum=False, model="hyper"):

@@ -104,3 +104,27 @@ def test_attack_rd_cli_runs(capsys):
     txt = capsys.readouterr().out
     assert "AVG: hyper-mse-1" in txt and "synthetic_0" in txt and "synthetic_1" in txt
     assert out["bpp_ori"] > 0 and out["bpp"] > 0
+
+
+def test_attack_rd_cli_targeted_roi(capsys, tmp_path, monkeypatch):
+    """-t / --mask_loc (README 'attack with ROI'): runs end to end and writes the target-suffixed PNGs."""
+    from imagecompression_adversarial_amd import attack_rd, coder
+    monkeypatch.chdir(tmp_path)
+    args = coder.config().parse_args(["-m", "hyper", "-metric", "mse", "-q", "3", "-steps", "3", "-t", "synthetic",
+                                      "--mask_loc", "16", "96", "8", "64", "-la_bkg_in", "0.01",
+                                      "-s", "synthetic:1x128x128", "--synthetic-weights"])
+    out = attack_rd.main(args)
+    txt = capsys.readouterr().out
+    assert "-> synthetic" in txt and "AVG: hyper-mse-3" in txt
+    assert out["bpp"] > 0
+    assert any(p.name.endswith("_advin_synthetic.png") for p in tmp_path.iterdir())
+
+
+def test_cheng2020_cli_runs(capsys):
+    from imagecompression_adversarial_amd import attack_rd, coder
+    args = coder.config().parse_args(["-m", "cheng2020", "-metric", "ms-ssim", "-q", "6", "-steps", "2",
+                                      "-s", "synthetic:2x192x192", "--synthetic-weights", "--batch", "2"])
+    out = attack_rd.main(args)
+    txt = capsys.readouterr().out
+    assert "AVG: cheng2020-ms-ssim-6" in txt
+    assert out["bpp_ori"] > 0
