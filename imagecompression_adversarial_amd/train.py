@@ -74,8 +74,9 @@ def main_parameters(net):
     return [p for n, p in net.named_parameters() if not n.endswith(".quantiles")]
 
 
-def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, group=None, world=1):
-    """One outer step of train.py:335-366 on this rank's shard; grads averaged over ranks."""
+def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, group=None, world=1, qnoise=None):
+    """One outer step of train.py:335-366 on this rank's shard; grads averaged over ranks.
+    qnoise: optional (noise_y, noise_z) train-mode quantisation noise for this shard (tests)."""
     batch_x = batch_x.detach().contiguous()
     for p in net.parameters():
         p.requires_grad_(False)
@@ -90,7 +91,7 @@ def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, g
     net.train()
     optimizer.zero_grad(set_to_none=False)
     aux_optimizer.zero_grad()
-    out = trainer.step(batch_adv)
+    out = trainer.step(batch_adv, *(qnoise or ()))
     D.allreduce_mean_(trainer.flat_grad, group, world)
     torch.nn.utils.clip_grad_norm_(main_parameters(net), 1.0)
     optimizer.step()

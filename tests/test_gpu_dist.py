@@ -1,0 +1,103 @@
+"""Data-parallel adversarial fine-tune on the GPU: two ranks on the box's one GPU, gloo
+process group (RCCL needs one GPU per rank; the collective calls are the same).  One outer step of
+train.py --adv on two half-batch shards must equal one step on the whole batch in one process: the
+batch-coupled inner attack (4-byte all-reduce per inner step), the gradient mean (one flat all-reduce),
+clip + Adam.  Ranks must end bit-identical to each other."""
+import os
+import socket
+from types import SimpleNamespace
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, H, W = 4, 128, 128
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs():
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand((B, 3, H, W), generator=g)
+    ny = torch.rand((B, 192, H // 16, W // 16), generator=g) - 0.5
+    nz = torch.rand((B, 128, H // 64, W // 64), generator=g) - 0.5
+    return x, ny, nz
+
+
+def _args():
+    return SimpleNamespace(steps=3, epsilon=16.0, noise=1e-4, lr_attack=0.01, att_metric="L2", clamp=True,
+                           round_adv=False)
+
+
+def _one_step(rank, world, group):
+    from imagecompression_adversarial_amd import codec, coder
+    from imagecompression_adversarial_amd.train import adv_step
+    from imagecompression_adversarial_amd.train_engine import RDTrainer
+    from imagecompression_adversarial_amd import dist as D
+    net = codec.bmshj2018_hyperprior(3)
+    coder._synthetic_init(net, seed=0)
+    net = net.to("cuda:0").train()
+    opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=1e-4))
+    tr = RDTrainer(net, "mse", 0.0130)
+    x, ny, nz = _inputs()
+    sl = D.shard_range(B, rank, world)
+    sh = slice(sl.start, sl.stop)
+    out, _ = adv_step(net, tr, opt, aux, x[sh].cuda(), _args(), group, world,
+                      qnoise=(ny[sh].cuda(), nz[sh].cuda()))
+    torch.cuda.synchronize()
+    flat = torch.cat([p.detach().flatten() for p in net.parameters()]).cpu()
+    return flat, float(out["loss"])
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    try:
+        from imagecompression_adversarial_amd import dist as D
+        torch.cuda.set_device(0)
+        r, w, group = D.init_from_env("gloo")
+        flat, loss = _one_step(r, w, group)
+        q.put((rank, flat, loss, None))
+    except Exception as e:  # surface failures to the parent
+        q.put((rank, None, None, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_dp_adv_step_matches_single_process():
+    ref_flat, ref_loss = _one_step(0, 1, None)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, flat, loss, err = q.get(timeout=300)
+        assert err is None, err
+        res[rank] = (flat, loss)
+    for p in procs:
+        p.join(timeout=60)
+    assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
+    d = (res[0][0] - ref_flat).abs().max().item()
+    moved = (ref_flat - _init_flat()).abs().max().item()
+    assert moved > 0
+    assert d <= 2e-3 * moved, (d, moved)
+    # each rank reports its shard's loss; the whole-batch loss is their mean
+    assert abs(0.5 * (res[0][1] + res[1][1]) - ref_loss) <= 1e-3 * abs(ref_loss)
+
+
+def _init_flat():
+    from imagecompression_adversarial_amd import codec, coder
+    net = codec.bmshj2018_hyperprior(3)
+    coder._synthetic_init(net, seed=0)
+    return torch.cat([p.detach().flatten() for p in net.parameters()])
