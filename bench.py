@@ -1,5 +1,7 @@
 """Benchmark: attack-step·images/s on Balle2018-hyperprior q3, 512x768 (BASELINE.json configs[1]);
-``--model cheng2020`` measures configs[2]'s per-GPU shard (cheng2020-anchor q6, 32 images of 768x512).
+``--model cheng2020`` measures configs[2]'s per-GPU shard (cheng2020-anchor q6, 32 images of 768x512);
+``--config 5`` measures configs[4]'s per-GPU shard: the targeted ROI attack on 2048x2048 tiles on the
+bf16-operand MFMA conv path (8 tiles per GPU, target = a second synthetic image, ROI = the centre box).
 
 One "step" = one attack_rd.attack_ iteration over the per-GPU batch: L-inf box
 + input clamp, g_a + g_s forward, loss, g_s + g_a input-gradient backward, Adam
@@ -27,6 +29,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "attack-step·images/sec, Balle2018-hyper 768×512 1001-step PGD, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA, dense (no sparsity)
 
 
 def layer_flops(tag, N, M, H, W, B):
@@ -93,6 +96,18 @@ def cpu_baseline(H, W, quality, seconds, model="hyper"):
                       f"{model} q{quality}, {n} timed steps after 1 warm-up ({el:.1f} s)"}
 
 
+def _bf16_tags(kern):
+    """Tags of the conv launches that run on bf16 operands (the roofline peak for those is BF16 MFMA)."""
+    tags = set()
+    for tr, pre in ((kern.ga, "g_a"), (kern.gs, "g_s")):
+        for i, p in enumerate(tr.convs):
+            if p.fwd_prec:
+                tags.add(f"{pre}.{2 * i}.fwd")
+            if p.bwd_prec:
+                tags.add(f"{pre}.{2 * i}.dgrad")
+    return tags
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,10 +118,29 @@ def main():
     ap.add_argument("--width", type=int, default=768)
     ap.add_argument("--quality", type=int, default=None, help="default 3 (hyper) / 6 (cheng2020)")
     ap.add_argument("--model", default="hyper", choices=("hyper", "cheng2020"))
+    ap.add_argument("--precision", default=None, choices=("fp32", "bf16"),
+                    help="conv operand precision of g_a/g_s (default fp32; bf16 for --config 5)")
+    ap.add_argument("--config", type=int, default=None, choices=(2, 3, 5),
+                    help="BASELINE.json configs[k-1] per-GPU shard: 2 hyper q3 fp32 (default), 3 cheng2020 q6, "
+                         "5 targeted ROI hyper q3 2048x2048 bf16")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    roi_mode = False
+    if args.config == 3:
+        args.model = "cheng2020"
+    elif args.config == 5:
+        roi_mode = True
+        args.height = args.width = 2048
+        if args.batch == 32:
+            args.batch = 8
+        if args.precision is None:
+            args.precision = "bf16"
+    if args.precision is None:
+        args.precision = "fp32"
+    if args.precision == "bf16" and args.model != "hyper":
+        raise SystemExit("the bf16 conv path covers the bmshj2018 transforms (config 5)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -117,7 +151,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from oracle import codec  # synthetic CompressAI-format weights (seeded), not the checker here
+    from imagecompression_adversarial_amd import codec as models
     from imagecompression_adversarial_amd import hip_ops as K
     from imagecompression_adversarial_amd.attack import AttackLoop
     from imagecompression_adversarial_amd.engine import CodecKernels
@@ -127,13 +161,19 @@ def main():
     model = args.model
     if args.quality is None:
         args.quality = 6 if model == "cheng2020" else 3
-    P = codec.init_params(model, args.quality, seed=0)
-    sd = {k: v.to(dev) for k, v in P.items()}
-    kern = ChengKernels(sd) if model == "cheng2020" else CodecKernels(sd, "hyper")
+    # random-init CompressAI-architecture weights (seed 0; no checkpoints offline), product modules
+    torch.manual_seed(0)
+    net = models.cheng2020_anchor(args.quality) if model == "cheng2020" else models.bmshj2018_hyperprior(args.quality)
+    sd = {k: v.detach().to(dev) for k, v in net.state_dict().items()}
+    kern = ChengKernels(sd) if model == "cheng2020" else CodecKernels(sd, "hyper", precision=args.precision)
     N, M = kern.N, kern.M
     gen = torch.Generator(device=dev).manual_seed(rank)
     im_s = torch.rand((B, 3, H, W), generator=gen, device=dev)
-    loop = AttackLoop(kern, im_s, steps=1001)
+    roi_kw = {}
+    if roi_mode:   # README "attack with ROI": -t target, --mask_loc x0 x1 y0 y1 (centre box), la_* defaults
+        roi_kw = dict(target=torch.rand((B, 3, H, W), generator=gen, device=dev),
+                      roi=(W // 4, 3 * W // 4, H // 4, 3 * H // 4), la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0)
+    loop = AttackLoop(kern, im_s, steps=1001, **roi_kw)
 
     for i in range(args.warmup):
         loop.step(i)
@@ -166,9 +206,10 @@ def main():
         flops_of = {t: layer_flops(t, N, M, H, W, B) for t in per_tag}
     dom_flops = flops_of[dom]
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+    peak = BF16_MFMA_PEAK_TFLOPS if (args.precision == "bf16" and dom in _bf16_tags(kern)) else FP32_MFMA_PEAK_TFLOPS
     traffic = None
     tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
+    if os.path.exists(tf) and args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32):
         try:
             traffic = json.load(open(tf)).get(dom)
         except Exception:
@@ -184,23 +225,31 @@ def main():
             cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds, model)
         metric = METRIC if model == "hyper" else \
             "attack-step·images/sec, Cheng2020-anchor q6 768×512 (configs[2] per-GPU shard)"
+        if roi_mode:
+            metric = "attack-step·images/sec, targeted ROI attack Balle2018-hyper 2048×2048 bf16 (configs[4] per-GPU shard)"
         name = "hyper" if model == "hyper" else "cheng2020"
         out = {
             "metric": metric, "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 operands, f32 accumulate" if args.precision == "bf16" else "f32",
             "data": "synthetic (torch.rand images, seeded CompressAI-init weights)",
-            "config": {"workload": f"attack_rd -m {name} -q {args.quality} -att_metric L2 -noise 1e-4, "
-                                   f"{B} images/GPU of {W}x{H}, steps of the 1001-step loop",
+            "config": {"workload": (f"attack_rd -m {name} -q {args.quality} -att_metric L2 -noise 1e-4"
+                                    + (f" -t <target> --mask_loc {W // 4} {3 * W // 4} {H // 4} {3 * H // 4}"
+                                       if roi_mode else "")
+                                    + f", {B} images/GPU of {W}x{H}, steps of the 1001-step loop, "
+                                      f"{args.precision} conv operands"),
                        "per_gpu_batch": B, "global_batch": B * world, "height": H, "width": W,
                        "parallelism": f"image-shard x{world} (no data-path collective)"},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
                          "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
             "step_gflop_per_image": round(total_flops / B / 1e9, 2),
             "step_tflops": round(total_flops / (ms_step * 1e-3) / 1e12, 2),
-            "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+            "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 /
+                                        (BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS),
+                                        4),
             "per_kernel_ms": {k: round(v, 4) for k, v in sorted(per_tag.items())},
             "cpu_baseline": cpu,
         }

@@ -27,8 +27,10 @@ _SIGS = {
     "ica_conv_it": [_i],
     "ica_pack_conv_weight_size": [_i, _i, _i, _i, _i],
     "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _i, _p],
+    "ica_pack_conv_weight_bf16": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
+    "ica_pack_gdn_bf16": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_up3_size": [_i],
     "ica_pack_up3": [_p, _p, _i, _p],
     "ica_conv_up3": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
@@ -86,7 +88,7 @@ class ConvArgs(C.Structure):
     _fields_ = ([(n, C.c_void_p) for n in ("x", "y", "wp", "bias", "gp", "beta", "save_x", "save_s", "in_x", "in_s",
                                             "save_t", "res", "mask")]
                 + [(n, C.c_int) for n in ("N", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kind", "KS", "S", "epi",
-                                           "it", "fill_mode", "ps")])
+                                           "it", "fill_mode", "ps", "prec")])
 
 
 _lib = None

@@ -20,6 +20,58 @@ ICA_DEV f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_32x32x16_bf16: lane l (r = l&31, h = l>>5) supplies A[r][k = 8h + j], B[k = 8h + j][r]
+// in element j = 0..7; the D layout is that of the f32 form (dtype-independent on gfx950).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+ICA_DEV f32x16 mfma32bf(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// 8 fp32 -> 8 bf16 (round to nearest even: v_cvt_pk_bf16_f32)
+ICA_DEV bf16x8 to_bf8(f32x4 lo, f32x4 hi) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r[e] = (__bf16)lo[e];
+    r[4 + e] = (__bf16)hi[e];
+  }
+  return r;
+}
+// v = hi + lo + O(2^-16 |v|): the two-term bf16 split of a fp32 operand (bf16x3 products)
+ICA_DEV void split_bf(float v, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)v;
+  lo = (__bf16)(v - (float)hi);
+}
+// Buffer-descriptor loads of wave-uniform tables (32-bit lane offset + scalar/immediate offset, so
+// the compiler keeps no per-fragment 64-bit address registers live).
+ICA_DEV __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+ICA_DEV bf16x8 ld_bf8(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+// Per-image view of an nChw4c tensor through a buffer descriptor (n is block-uniform): a 32-bit lane
+// offset (voff) plus a wave-uniform scalar offset (soff), so an epilogue keeps no 64-bit per-element
+// address registers live (those spilled in the GDN-backward epilogue).  One image must be < 4 GiB.
+struct Img4 {
+  __amdgpu_buffer_rsrc_t r;
+  ICA_DEV Img4(const float* base, size_t img_floats, int n)
+      : r(uniform_rsrc(base ? base + (size_t)n * img_floats : base, (unsigned)(img_floats * 4))) {}
+  ICA_DEV f32x4 ld(unsigned voff, unsigned soff) const {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+  }
+  // Stores fold the scalar offset into voff and pass a constant soffset 0.  With an SGPR soffset, hipcc
+  // (ROCm 7.2) omits the wait state between a >8-byte buffer store and a VALU overwrite of its data
+  // registers (LLVM models that hazard only for a constant soffset); on gfx950 the overwrite then
+  // corrupted dword 1 of lanes 12-15 of each 16-lane group (measured: conv_up IGDN save_s).
+  ICA_DEV void st(unsigned voff, unsigned soff, f32x4 v) const {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(voff + soff), 0, 0);
+  }
+};
+ICA_DEV f32x4 bf8_as_f4(bf16x8 v) { return __builtin_bit_cast(f32x4, v); }
+ICA_DEV bf16x8 f4_as_bf8(f32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
 // Row index (within a 32-row tile) held by accumulator register r of lane half h.
 ICA_DEV constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 

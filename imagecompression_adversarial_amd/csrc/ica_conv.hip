@@ -60,6 +60,9 @@ struct ConvParams {
   const float* mask;  // conv_down fill_mode 1: leaky-ReLU mask source (input layout)
   int fill_mode;      // conv_down: 0 plain, 1 x * lrelu'(mask), 2 PixelUnshuffle(2) view of x
   int ps;             // PixelShuffle(2) store (BIAS/RELU/LRELU epilogues)
+  int prec;           // 0: fp32 operands (v_mfma_f32_32x32x2_f32, exact fp32 products)
+                      // 1: bf16 operands, fp32 accumulate (v_mfma_f32_32x32x16_bf16); wp / gp hold the
+                      //    bf16 packs (ica_pack_conv_weight_bf16 / ica_pack_gdn_bf16)
 };
 
 // --------------------------------------------------------------------------
@@ -67,23 +70,32 @@ struct ConvParams {
 // (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
 // float4 of channel group c4 = co_base/4 + it*8 + 2g + h.
 // --------------------------------------------------------------------------
-template <int IT, int EPI, int FX>
+template <int IT, int EPI, int FX, bool BF = false>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
                            bool valid, int co_base) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int C4o = (p.Cout + 3) >> 2;
-  const size_t plane = (size_t)p.Hout * p.Wout;
-  const size_t pix = valid ? ((size_t)oy * p.Wout + ox) : 0;
-  auto off = [&](int c4) -> size_t { return (((size_t)n * C4o + c4) * plane + pix) * 4; };
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const unsigned pix = valid ? ((unsigned)oy * p.Wout + ox) : 0u;
+  const size_t img = (size_t)C4o * plane * 4;  // floats per image of every output-layout tensor
+  // channel group c4 = u + h (u = co_base/4 + it*8 + 2g, wave-uniform): byte offset = vo + so(u)
+  const unsigned vo = (h * plane + pix) * 16u;
+  auto so = [&](int u) -> unsigned { return (unsigned)u * plane * 16u; };
+  const int cu = co_base >> 2;
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_LRELU) {
-    // PixelShuffle(2) store: output tensor [N][Cout/16][2 Hout][2 Wout][4]
-    const size_t plane2 = 4 * plane;
-    const size_t pix2 = valid ? ((size_t)(2 * oy) * (2 * p.Wout) + 2 * ox) : 0;
-    auto off_ps = [&](int c0) -> size_t {
-      const int c4 = c0 >> 4, q = (c0 >> 2) & 3;
-      return (((size_t)n * (p.Cout >> 4) + c4) * plane2 + pix2 + (size_t)(q >> 1) * (2 * p.Wout) + (q & 1)) * 4;
+    const Img4 Y(p.y, img, n);
+    // PixelShuffle(2) store: output tensor [N][Cout/16][2 Hout][2 Wout][4]; rho-row quad (it, g, h) is
+    // channel group c4 = (cu + it*8 + 2g) / 4 at sub-pixel q = 2(g&1) + h of the (2Hout)x(2Wout) plane
+    const unsigned plane2 = 4u * plane;
+    const unsigned vo_ps = (valid ? ((unsigned)(2 * oy) * (2 * p.Wout) + 2 * ox + h) : 0u) * 16u;
+    auto so_ps = [&](int it, int g) -> unsigned {
+      const int c4 = (cu + it * 8 + 2 * g) >> 2;
+      return ((unsigned)c4 * plane2 + (unsigned)(g & 1) * (2 * p.Wout)) * 16u;
     };
+    // (the shuffled tensor holds the same Cout * Hout * Wout floats per image as the plain one)
+    const Img4 SX((FX & FX_RES) ? p.save_x : nullptr, img, n);
+    const Img4 RS((FX & FX_RES) ? p.res : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
@@ -104,47 +116,73 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           v[e] = t;
         }
         if (valid) {
-          size_t o;
-          if constexpr ((FX & FX_PS) != 0) o = off_ps(c0);
-          else o = off(c0 >> 2);
+          unsigned vv, ss;
+          if constexpr ((FX & FX_PS) != 0) {
+            vv = vo_ps;
+            ss = so_ps(it, g);
+          } else {
+            vv = vo;
+            ss = so(cu + it * 8 + 2 * g);
+          }
           if constexpr ((FX & FX_RES) != 0) {
-            if (p.save_x) st4(p.save_x + o, v);
+            if (p.save_x) SX.st(vv, ss, v);
             if (p.res) {
-              const f32x4 r = ld4(p.res + o);
+              const f32x4 r = RS.ld(vv, ss);
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] += r[e];
             }
           }
-          st4(p.y + o, v);
+          Y.st(vv, ss, v);
         }
       }
     }
   } else if constexpr (EPI == EPI_LRELU_BWD) {
+    const Img4 Y(p.y, img, n), M(p.in_x, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c0 = co_base + it * 32 + 8 * g + 4 * h;
         if (c0 >= p.Cout || !valid) continue;
-        const size_t o = off(c0 >> 2);
-        const f32x4 m = ld4(p.in_x + o);
+        const unsigned ss = so(cu + it * 8 + 2 * g);
+        const f32x4 m = M.ld(vo, ss);
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float t = acc[it][4 * g + e];
           v[e] = (c0 + e < p.Cout) ? (m[e] > 0.f ? t : t * 0.01f) : 0.f;
         }
-        st4(p.y + o, v);
+        Y.st(vo, ss, v);
       }
     }
   } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
     // requires IT*32 == Cout, co_base == 0.  acc := x = conv + bias (kept intact
     // until every normaliser tile is done); one 32-channel tile of
     // n = beta' + gamma' x^2 at a time (16 accumulator registers live).
+    const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+    const Img4 SX((FX & FX_RES) ? p.save_x : nullptr, img, n), RS((FX & FX_RES) ? p.res : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
+    // bf16 path: x^2 as the B operand of a bf16x3 GEMM (hi*hi + lo*hi + hi*lo), the accumulator
+    // registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives the matching gamma' order)
+    bf16x8 xh[BF ? IT : 1][2], xl[BF ? IT : 1][2];
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
+    if constexpr (BF) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xv = acc[it][8 * s + j];
+            __bf16 hi, lo;
+            split_bf(xv * xv, hi, lo);
+            xh[it][s][j] = hi;
+            xl[it][s][j] = lo;
+          }
+    }
 #pragma unroll
     for (int ct = 0; ct < IT; ++ct) {
       f32x16 nacc;
@@ -152,14 +190,25 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       for (int r = 0; r < 16; ++r) nacc[r] = p.beta[ct * 32 + acc_row(r, h)];
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
-        const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-        const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                              g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+        if constexpr (BF) {
+          const int o = (ct * IT + it) * 4096;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float xv = acc[it][r];
-          nacc = mfma32(ga[r], xv * xv, nacc);
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
+            nacc = mfma32bf(ah, xh[it][s], nacc);
+            nacc = mfma32bf(al, xh[it][s], nacc);
+            nacc = mfma32bf(ah, xl[it][s], nacc);
+          }
+        } else {
+          const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
+          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float xv = acc[it][r];
+            nacc = mfma32(ga[r], xv * xv, nacc);
+          }
         }
       }
       if (valid) {
@@ -173,17 +222,17 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
             sv[e] = s;
             yv[e] = acc[ct][4 * g + e] * s;
           }
-          const size_t o = off(ct * 8 + 2 * g + h);
-          if (p.save_s) st4(p.save_s + o, sv);
+          const unsigned ss = so(ct * 8 + 2 * g);
+          if (p.save_s) SS.st(vo, ss, sv);
           if constexpr ((FX & FX_RES) != 0) {
-            if (p.save_x) st4(p.save_x + o, yv);
+            if (p.save_x) SX.st(vo, ss, yv);
             if (p.res) {
-              const f32x4 r = ld4(p.res + o);
+              const f32x4 r = RS.ld(vo, ss);
 #pragma unroll
               for (int e = 0; e < 4; ++e) yv[e] += r[e];
             }
           }
-          st4(p.y + o, yv);
+          Y.st(vo, ss, yv);
         }
       }
     }
@@ -193,18 +242,20 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // accumulators) and dx = g s + 2 x u with x, s re-read (L2-hot).
     // Residual gradient: added unconditionally (r = 0 without one) so that the accumulators are
     // never live in two versions across a branch (that doubled the register footprint).
+    const Img4 Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
     if constexpr ((FX & FX_RES) != 0) {
+      const Img4 SX(p.save_x, img, n), RS(p.res, img, n);
 #pragma unroll
       for (int it = 0; it < IT; ++it)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const size_t o = off(it * 8 + 2 * g + h);
+          const unsigned ss = so(it * 8 + 2 * g);
           f32x4 r = {0.f, 0.f, 0.f, 0.f};
-          if (p.res && valid) r = ld4(p.res + o);
+          if (p.res && valid) r = RS.ld(vo, ss);
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
           if (p.save_x && valid)
-            st4(p.save_x + o, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+            SX.st(vo, ss, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
         }
     }
     // IT > 4 (C = 192): g*s is parked in the output (same-thread global write, re-read below) so that
@@ -216,23 +267,24 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         for (int it = 0; it < IT; ++it)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const size_t o = off(it * 8 + 2 * g + h);
-            const f32x4 sv = ld4(p.in_s + o);
-            st4(p.y + o, f32x4{acc[it][4 * g] * sv[0], acc[it][4 * g + 1] * sv[1], acc[it][4 * g + 2] * sv[2],
+            const unsigned ss = so(it * 8 + 2 * g);
+            const f32x4 sv = IS.ld(vo, ss);
+            Y.st(vo, ss, f32x4{acc[it][4 * g] * sv[0], acc[it][4 * g + 1] * sv[1], acc[it][4 * g + 2] * sv[2],
                                acc[it][4 * g + 3] * sv[3]});
           }
       }
     }
     f32x16 tt[IT];
+    const Img4 ST((FX & FX_T) ? p.save_t : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
+        const unsigned ss = so(it * 8 + 2 * g);
         f32x4 xv = {0.f, 0.f, 0.f, 0.f}, sv = {1.f, 1.f, 1.f, 1.f};
         if (valid) {
-          const size_t o = off(it * 8 + 2 * g + h);
-          xv = ld4(p.in_x + o);
-          sv = ld4(p.in_s + o);
+          xv = IX.ld(vo, ss);
+          sv = IS.ld(vo, ss);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -241,31 +293,51 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
         }
         if constexpr ((FX & FX_T) != 0) {
-          if (valid)
-            st4(p.save_t + off(it * 8 + 2 * g + h),
-                f32x4{tt[it][4 * g], tt[it][4 * g + 1], tt[it][4 * g + 2], tt[it][4 * g + 3]});
+          if (valid) ST.st(vo, ss, f32x4{tt[it][4 * g], tt[it][4 * g + 1], tt[it][4 * g + 2], tt[it][4 * g + 3]});
         }
       }
+    // bf16: t is split into hi/lo B fragments on the fly per (jt, ct) (keeping all IT*4 split fragments
+    // live beside acc and t does not fit 256 registers)
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) {
       f32x16 uacc = f32x16{0};
 #pragma unroll
       for (int ct = 0; ct < IT; ++ct) {
-        const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
-        const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-        const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                              g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+        if constexpr (BF) {
+          const int o = (jt * IT + ct) * 4096;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
+            bf16x8 th, tl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              __bf16 hi, lo;
+              split_bf(tt[ct][8 * s + j], hi, lo);
+              th[j] = hi;
+              tl[j] = lo;
+            }
+            uacc = mfma32bf(ah, th, uacc);
+            uacc = mfma32bf(al, th, uacc);
+            uacc = mfma32bf(ah, tl, uacc);
+          }
+        } else {
+          const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
+          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+#pragma unroll
+          for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+        }
       }
       if (valid) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const size_t o = off(jt * 8 + 2 * g + h);
-          const f32x4 xv = ld4(p.in_x + o), sv = ld4(p.in_s + o);
+          const unsigned ss = so(jt * 8 + 2 * g);
+          const f32x4 xv = IX.ld(vo, ss), sv = IS.ld(vo, ss);
           f32x4 v;
           if constexpr (STASH) {
-            const f32x4 gs = ld4(p.y + o);
+            const f32x4 gs = Y.ld(vo, ss);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * (xv[e] / sv[e]) * uacc[4 * g + e];
           } else {
@@ -275,7 +347,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
               v[e] = acc[jt][r] * sv[e] + 2.0f * (xv[e] / sv[e]) * uacc[r];
             }
           }
-          st4(p.y + o, v);
+          Y.st(vo, ss, v);
         }
       }
     }
@@ -315,13 +387,17 @@ ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
 // [cb][chunk][tap][it][lane][KH]  with  o = cb*IT*32 + it*32 + (lane&31),
 // c = chunk*CC + (lane>>5)*KH + s.
 // --------------------------------------------------------------------------
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
 __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   constexpr int TH = 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
   constexpr int NQ = CC / 4, KH = CC / 2, PLANE = PR * PC, PAD = KS / 2;
   constexpr int WSTEP = IT * 64 * KH;  // floats per (chunk, tap)
-  __shared__ f32x4 patch[NQ * PLANE];
+  // bf16 operands (BF): one 16-B LDS entry holds 8 channels of a pixel as bf16 (2 entries per
+  // 16-channel chunk, entry h = channels 8h..8h+7 = the B fragment of lane half h)
+  constexpr int NE = BF ? NQ / 2 : NQ;
+  static_assert(!BF || CC == 16, "bf16 conv_down needs 16-channel chunks");
+  __shared__ f32x4 patch[NE * PLANE];
 
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
   int bid = blockIdx.x;
@@ -341,85 +417,132 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 #pragma unroll
   for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
 
-  // Weight fragments stream linearly through (chunk, tap); they are prefetched
-  // one tap ahead into the other of two register sets (ping-pong, no copies)
-  // so each tap's MFMAs cover the next tap's global (L2-resident) load latency.
-  const float* wptr = p.wp + (size_t)cb * nch * KS * KS * WSTEP + (size_t)lane * KH;
+  // one 4-channel group of the conv input at (iy, ix), with the fill-mode view applied
+  auto ldc4 = [&](int c4, int iy, int ix) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#ifdef ICA_ABLATE_FILL
+    if (false) {
+#else
+    if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
+#endif
+      if constexpr ((FX & FX_UNSHUF) != 0) {
+        // PixelUnshuffle(2): rho channel 16*c4g + 4*q + e of pixel (iy, ix) is channel 4*c4g + e
+        // of the (2 Hin) x (2 Win) tensor at sub-pixel q = 2i + j
+        const int c4g = c4 >> 2, q = c4 & 3;
+        v = ld4(p.x + ((((size_t)n * (Cin4 >> 2) + c4g) * (2 * p.Hin) + 2 * iy + (q >> 1)) * (2 * p.Win) +
+                       2 * ix + (q & 1)) * 4);
+      } else {
+        const size_t xo = ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4;
+        v = ld4(p.x + xo);
+        if constexpr ((FX & FX_MASK) != 0) {
+          const f32x4 m = ld4(p.mask + xo);
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) v[e2] = m[e2] > 0.f ? v[e2] : v[e2] * 0.01f;
+        }
+      }
+      if constexpr (CC == 4) {
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2)
+          if (c4 * 4 + e2 >= p.Cin) v[e2] = 0.f;
+      }
+    }
+    return v;
+  };
+  auto fill = [&](int ch) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < NE * PLANE; e += 256) {
+      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+      const int iy = iy0 + pr, ix = ix0 + pc;
+      if constexpr (BF) {
+        const int c4 = ch * NQ + 2 * q;
+        patch[e] = bf8_as_f4(to_bf8(ldc4(c4, iy, ix), ldc4(c4 + 1, iy, ix)));
+      } else {
+        patch[e] = ldc4(ch * NQ + q, iy, ix);
+      }
+    }
+    __syncthreads();
+  };
+
   constexpr int KK = KS * KS;
   const int total = nch * KK;
   const int lbase = (S * oyl) * PC + S * oxl;
-  auto step = [&](float (&cur)[IT][KH], float (&nxt)[IT][KH], int g) {
-    const int ch = g / KK, tap = g - ch * KK;
-    if (tap == 0) {
-      __syncthreads();
-      for (int e = threadIdx.x; e < NQ * PLANE; e += 256) {
-        const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
-        const int c4 = ch * NQ + q, iy = iy0 + pr, ix = ix0 + pc;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-#ifdef ICA_ABLATE_FILL
-        if (false) {
-#else
-        if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
-#endif
-          if constexpr ((FX & FX_UNSHUF) != 0) {
-            // PixelUnshuffle(2): rho channel 16*c4g + 4*q + e of pixel (iy, ix) is channel 4*c4g + e
-            // of the (2 Hin) x (2 Win) tensor at sub-pixel q = 2i + j
-            const int c4g = c4 >> 2, q = c4 & 3;
-            v = ld4(p.x + ((((size_t)n * (Cin4 >> 2) + c4g) * (2 * p.Hin) + 2 * iy + (q >> 1)) * (2 * p.Win) +
-                           2 * ix + (q & 1)) * 4);
-          } else {
-            const size_t xo = ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4;
-            v = ld4(p.x + xo);
-            if constexpr ((FX & FX_MASK) != 0) {
-              const f32x4 m = ld4(p.mask + xo);
+  if constexpr (BF) {
+    // bf16: one v_mfma_f32_32x32x16_bf16 per (chunk, tap, tile) = 32 cycles, so the weight
+    // fragments (16 B per lane per tile, L2-resident) are prefetched 3 steps ahead in a 4-set
+    // register ring (indices compile-time via a 4x unrolled loop: no scratch, no copies).
+    const bf16x8* wb = reinterpret_cast<const bf16x8*>(p.wp) + (size_t)cb * nch * KK * IT * 64 + lane;
+    bf16x8 fr[4][IT];
+    auto ldw = [&](bf16x8 (&a)[IT], int g) {
+      const bf16x8* w = wb + (size_t)min(g, total - 1) * IT * 64;
 #pragma unroll
-              for (int e2 = 0; e2 < 4; ++e2) v[e2] = m[e2] > 0.f ? v[e2] : v[e2] * 0.01f;
-            }
-          }
-          if constexpr (CC == 4) {
+      for (int it = 0; it < IT; ++it) a[it] = w[it * 64];
+    };
+    auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int g) {
+      const int ch = g / KK, tap = g - ch * KK;
+      if (tap == 0) fill(ch);
+      ldw(nxt, g + 3);
+      const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+      const bf16x8 b = f4_as_bf8(patch[h * PLANE + lbase + ky * PC + kx]);
 #pragma unroll
-            for (int e2 = 0; e2 < 4; ++e2)
-              if (c4 * 4 + e2 >= p.Cin) v[e2] = 0.f;
-          }
-        }
-        patch[e] = v;
-      }
-      __syncthreads();
-    }
-    load_frag<IT, KH>(nxt, wptr + (size_t)min(g + 1, total - 1) * WSTEP);  // unconditional: no phi copies
-    const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-    const int lo = lbase + ky * PC + kx;
-    float b[KH];
-    if constexpr (CC == 16) {
-      const f32x4 v0 = patch[(2 * h) * PLANE + lo];
-      const f32x4 v1 = patch[(2 * h + 1) * PLANE + lo];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        b[e] = v0[e];
-        b[4 + e] = v1[e];
-      }
-    } else {  // CC == 4
-      const float* pf = reinterpret_cast<const float*>(&patch[lo]) + 2 * h;
-      const f32x2 v = *reinterpret_cast<const f32x2*>(pf);
-      b[0] = v[0];
-      b[1] = v[1];
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < KH; ++s2)
-#pragma unroll
-      for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
-  };
-  float fa[IT][KH], fb[IT][KH];
-  load_frag<IT, KH>(fa, wptr);
-  int g = 0;
+      for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], b, acc[it]);
+    };
+    ldw(fr[0], 0);
+    ldw(fr[1], 1);
+    ldw(fr[2], 2);
+    int g = 0;
 #pragma unroll 1
-  for (; g + 1 < total; g += 2) {
-    step(fa, fb, g);
-    step(fb, fa, g + 1);
+    for (; g + 4 <= total; g += 4) {
+      step(fr[0], fr[3], g);
+      step(fr[1], fr[0], g + 1);
+      step(fr[2], fr[1], g + 2);
+      step(fr[3], fr[2], g + 3);
+    }
+    if (g < total) step(fr[0], fr[3], g);
+    if (g + 1 < total) step(fr[1], fr[0], g + 1);
+    if (g + 2 < total) step(fr[2], fr[1], g + 2);
+  } else {
+    // Weight fragments stream linearly through (chunk, tap); they are prefetched
+    // one tap ahead into the other of two register sets (ping-pong, no copies)
+    // so each tap's MFMAs cover the next tap's global (L2-resident) load latency.
+    const float* wptr = p.wp + (size_t)cb * nch * KS * KS * WSTEP + (size_t)lane * KH;
+    auto step = [&](float (&cur)[IT][KH], float (&nxt)[IT][KH], int g) {
+      const int ch = g / KK, tap = g - ch * KK;
+      if (tap == 0) fill(ch);
+      load_frag<IT, KH>(nxt, wptr + (size_t)min(g + 1, total - 1) * WSTEP);  // unconditional: no phi copies
+      const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+      const int lo = lbase + ky * PC + kx;
+      float b[KH];
+      if constexpr (CC == 16) {
+        const f32x4 v0 = patch[(2 * h) * PLANE + lo];
+        const f32x4 v1 = patch[(2 * h + 1) * PLANE + lo];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          b[e] = v0[e];
+          b[4 + e] = v1[e];
+        }
+      } else {  // CC == 4
+        const float* pf = reinterpret_cast<const float*>(&patch[lo]) + 2 * h;
+        const f32x2 v = *reinterpret_cast<const f32x2*>(pf);
+        b[0] = v[0];
+        b[1] = v[1];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < KH; ++s2)
+#pragma unroll
+        for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+    };
+    float fa[IT][KH], fb[IT][KH];
+    load_frag<IT, KH>(fa, wptr);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 1 < total; g += 2) {
+      step(fa, fb, g);
+      step(fb, fa, g + 1);
+    }
+    if (g < total) step(fa, fb, g);
   }
-  if (g < total) step(fa, fb, g);
   const int oy = oy0 + oyl, ox = ox0 + oxl;
-  conv_epilogue<IT, EPI, FX>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  conv_epilogue<IT, EPI, FX, BF>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
 // --------------------------------------------------------------------------
@@ -433,7 +556,7 @@ constexpr int UP_TH = 4, UP_TW = 16, UP_PR = UP_TH + 2, UP_PC = UP_TW + 2, UP_PL
 // of a stride-2 KSxKS conv with pad KS/2 (KS = 5: g_s deconvs / g_a dgrad; KS = 3, 1: the dgrad of
 // cheng2020's conv3x3 s2 and conv1x1 s2 skips).  Output y = 2a + PY uses taps
 // ky = ky0 + 2i, ky0 = (PY + PAD) & 1, at input row iy = a + (PY + PAD - ky) / 2 in [a-1, a+1].
-template <int KS, int PY, int PX, int IT, int EPI, int FX>
+template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF>
 ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
                            int nch) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
@@ -442,49 +565,84 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
   constexpr int PAD = KS / 2;
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2;  // taps per axis
-  const float* wl = p.wp + (size_t)cb * KS * KS * nch * WSTEP + (size_t)lane * 8;
   f32x16 acc[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
-  // (tap, chunk) sequence flattened; weight fragments prefetched one step ahead
-  // into the other of two register sets (ping-pong).
+  // (tap, chunk) sequence flattened
   const int total = NY * NX * nch;
-  auto wptr = [&](int u) {
+  auto woff = [&](int u) -> size_t {
     const int ti = u / nch, ch = u - ti * nch;
-    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
-    return wl + ((size_t)(ky * KS + kx) * nch + ch) * WSTEP;
+    const int ky = KY0 + 2 * (ti / (NX > 0 ? NX : 1)), kx = KX0 + 2 * (ti % (NX > 0 ? NX : 1));
+    return (size_t)(ky * KS + kx) * nch + ch;
   };
-  auto step = [&](float (&cur)[IT][8], float (&nxt)[IT][8], int u) {
-    load_frag<IT, 8>(nxt, wptr(min(u + 1, total - 1)));  // unconditional: no phi copies
+  // LDS entry of (tap, chunk) step u for this lane: fp32 entries are 4 channels, bf16 entries 8
+  auto poff = [&](int u) -> int {
     const int ti = u / nch, ch = u - ti * nch;
-    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int ky = KY0 + 2 * (ti / (NX > 0 ? NX : 1)), kx = KX0 + 2 * (ti % (NX > 0 ? NX : 1));
     const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
-    const f32x4* pp = patch + (4 * ch + 2 * h) * UP_PLANE + pr * UP_PC + pc;
-    const f32x4 v0 = pp[0], v1 = pp[UP_PLANE];
-    const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2)
-#pragma unroll
-      for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+    return (BF ? (2 * ch + h) : (4 * ch + 2 * h)) * UP_PLANE + pr * UP_PC + pc;
   };
   if constexpr (NY * NX > 0) {
-    float fa[IT][8], fb[IT][8];
-    load_frag<IT, 8>(fa, wptr(0));
-    int u = 0;
+    if constexpr (BF) {
+      // bf16: 4-set weight-fragment ring, prefetch distance 3 (see conv_down_kernel)
+      const bf16x8* wb = reinterpret_cast<const bf16x8*>(p.wp) + (size_t)cb * KS * KS * nch * IT * 64 + lane;
+      bf16x8 fr[4][IT];
+      auto ldw = [&](bf16x8 (&a)[IT], int u) {
+        const bf16x8* w = wb + woff(min(u, total - 1)) * IT * 64;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) a[it] = w[it * 64];
+      };
+      auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int u) {
+        ldw(nxt, u + 3);
+        const bf16x8 b = f4_as_bf8(patch[poff(u)]);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], b, acc[it]);
+      };
+      ldw(fr[0], 0);
+      ldw(fr[1], 1);
+      ldw(fr[2], 2);
+      int u = 0;
 #pragma unroll 1
-    for (; u + 1 < total; u += 2) {
-      step(fa, fb, u);
-      step(fb, fa, u + 1);
+      for (; u + 4 <= total; u += 4) {
+        step(fr[0], fr[3], u);
+        step(fr[1], fr[0], u + 1);
+        step(fr[2], fr[1], u + 2);
+        step(fr[3], fr[2], u + 3);
+      }
+      if (u < total) step(fr[0], fr[3], u);
+      if (u + 1 < total) step(fr[1], fr[0], u + 1);
+      if (u + 2 < total) step(fr[2], fr[1], u + 2);
+    } else {
+      // weight fragments prefetched one step ahead into the other of two register sets (ping-pong)
+      const float* wl = p.wp + (size_t)cb * KS * KS * nch * WSTEP + (size_t)lane * 8;
+      auto step = [&](float (&cur)[IT][8], float (&nxt)[IT][8], int u) {
+        load_frag<IT, 8>(nxt, wl + woff(min(u + 1, total - 1)) * WSTEP);  // unconditional: no phi copies
+        const f32x4* pp = patch + poff(u);
+        const f32x4 v0 = pp[0], v1 = pp[UP_PLANE];
+        const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+          for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+      };
+      float fa[IT][8], fb[IT][8];
+      load_frag<IT, 8>(fa, wl + woff(0) * WSTEP);
+      int u = 0;
+#pragma unroll 1
+      for (; u + 1 < total; u += 2) {
+        step(fa, fb, u);
+        step(fb, fa, u + 1);
+      }
+      if (u < total) step(fa, fb, u);
     }
-    if (u < total) step(fa, fb, u);
   }
   const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
-  conv_epilogue<IT, EPI, FX>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  conv_epilogue<IT, EPI, FX, BF>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
-template <int KS, int IT, int EPI, int FX>
+template <int KS, int IT, int EPI, int FX, bool BF>
 __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
-  extern __shared__ f32x4 patch[];  // [Cin4][UP_PR][UP_PC]
+  extern __shared__ f32x4 patch[];  // fp32: [Cin/4][UP_PR][UP_PC] f32x4; bf16: [Cin/8][UP_PR][UP_PC] bf16x8
   const int Hh = p.Hin, Wh = p.Win;
   const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UP_TH - 1) / UP_TH;
   int bid = blockIdx.x;
@@ -495,13 +653,23 @@ __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   const int cb = blockIdx.y;
   const int a0 = ty * UP_TH, b0 = tx * UP_TW;
   const int Cin4 = p.Cin >> 2;  // Cin % 16 == 0 enforced by host
-  const int total = Cin4 * UP_PLANE;
+  const int total = (BF ? Cin4 / 2 : Cin4) * UP_PLANE;
   for (int e = threadIdx.x; e < total; e += 256) {
     const int q = e / UP_PLANE, rem = e - q * UP_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
     const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+    const bool ok = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+    const float* xp = p.x + ((((size_t)n * Cin4 + (BF ? 2 * q : q)) * p.Hin + iy) * p.Win + ix) * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win)
-      v = ld4(p.x + ((((size_t)n * Cin4 + q) * p.Hin + iy) * p.Win + ix) * 4);
+    if constexpr (BF) {
+      f32x4 v1 = v;
+      if (ok) {
+        v = ld4(xp);
+        v1 = ld4(xp + (size_t)p.Hin * p.Win * 4);
+      }
+      v = bf8_as_f4(to_bf8(v, v1));
+    } else {
+      if (ok) v = ld4(xp);
+    }
     patch[e] = v;
   }
   __syncthreads();
@@ -509,11 +677,13 @@ __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
   const int jt = wave & 1, nch = p.Cin / 16;
   // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
   if (wave < 2) {
-    conv_up_class<KS, 0, 0, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
-    conv_up_class<KS, 1, 1, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 0, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
+    conv_up_class<KS, 1, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   } else {
-    conv_up_class<KS, 0, 1, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
-    conv_up_class<KS, 1, 0, IT, EPI, FX>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, 0, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    __builtin_amdgcn_sched_barrier(0);
+    conv_up_class<KS, 1, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   }
 }
 
@@ -660,7 +830,8 @@ __global__ void pack_up3_kernel(const float* __restrict__ w, float* __restrict__
 //   order 0 (down): outer = chunk, inner = tap ; order 1 (up): outer = tap, inner = chunk
 //   o = cb*IT*32 + it*32 + (lane&31) ; c = chunk*CC + (lane>>5)*KH + s
 // value = w[o*so + c*sc + ky*KS + kx]  (0 outside O x C)
-__global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict__ dst, int O, int C, int KS,
+template <typename T>
+__global__ void pack_conv_kernel(const float* __restrict__ w, T* __restrict__ dst, int O, int C, int KS,
                                  long so, long sc, int IT, int CC, int order, long total, int flip) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
@@ -681,7 +852,7 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, float* __restrict_
   float v = 0.f;
   const int wt = flip ? KK - 1 - tap : tap;  // flip: spatially reversed kernel (dgrad of a stride-1 conv)
   if (o < O && c < C) v = w[o * so + c * sc + (wt / KS) * KS + (wt % KS)];
-  dst[i] = v;
+  dst[i] = (T)v;
 }
 
 // gamma' = max(gamma, 2^-18)^2 - 2^-36 ; beta' = max(beta, bound)^2 - 2^-36
@@ -712,6 +883,7 @@ __global__ void pack_gdn_kernel(const float* __restrict__ gamma, const float* __
   }
 }
 
+#ifndef ICA_KERNELS_ONLY  // (kernel-only builds: register/scratch experiments on single instantiations)
 // --------------------------------------------------------------------------
 // Host launchers (C ABI)
 // --------------------------------------------------------------------------
@@ -750,20 +922,27 @@ constexpr bool down_variant() {
 template <int KS, int S>
 constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) || (KS == 1 && S == 2); }
 
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
 static int launch_down(const ConvParams& p, hipStream_t st) {
   constexpr int TH = 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
-template <int KS, int S, int IT, int CC, int EPI, int FX>
+template <int KS, int S, int IT, int CC, int EPI, int FX, bool BF = false>
 static int pick_tw_down(const ConvParams& p, hipStream_t st) {
-  if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<KS, S, IT, CC, 32, EPI, FX>(p, st);
-  return launch_down<KS, S, IT, CC, 16, EPI, FX>(p, st);
+  if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<KS, S, IT, CC, 32, EPI, FX, BF>(p, st);
+  return launch_down<KS, S, IT, CC, 16, EPI, FX, BF>(p, st);
+}
+
+// bf16-operand variants: the bmshj2018 g_a forward / g_s input-gradient layers (k5 s2, 16-channel chunks)
+template <int KS, int S, int IT, int EPI, int FX>
+constexpr bool down_bf() {
+  return KS == 5 && S == 2 && FX == 0 && (IT == 3 || IT == 4) &&
+         (EPI == EPI_BIAS || EPI == EPI_GDN || EPI == EPI_IGDN_BWD);
 }
 
 template <int KS, int S, int IT, int EPI, int FX>
@@ -771,6 +950,13 @@ static int pick_cc_down(const ConvParams& p, hipStream_t st) {
   if constexpr (!down_variant<KS, S, IT, EPI, FX>()) {
     return -4;
   } else {
+    if (p.prec == 1) {
+      if constexpr (down_bf<KS, S, IT, EPI, FX>()) {
+        if (p.Cin <= 4) return -2;
+        return pick_tw_down<KS, S, IT, 16, EPI, FX, true>(p, st);
+      }
+      return -4;
+    }
     if (p.Cin <= 4) {
       if constexpr (down_cc4<KS, S>() && (FX == 0 || FX == FX_T)) return pick_tw_down<KS, S, IT, 4, EPI, FX>(p, st);
       return -2;
@@ -832,25 +1018,34 @@ static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, int fx
   return -6;
 }
 
-template <int KS, int IT, int EPI, int FX>
+template <int KS, int IT, int EPI, int FX, bool BF = false>
 static int launch_up(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  const size_t lds = (size_t)(p.Cin / 4) * UP_PLANE * sizeof(f32x4);
+  const size_t lds = (size_t)(p.Cin / (BF ? 8 : 4)) * UP_PLANE * sizeof(f32x4);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<KS, IT, EPI, FX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_kernel<KS, IT, EPI, FX, BF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_kernel<KS, IT, EPI, FX>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL((conv_up_kernel<KS, IT, EPI, FX, BF>), grid, dim3(256), lds, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStream_t st) {
+  if (p.prec == 1) {  // bf16 operands: the bmshj2018 g_s forward / g_a input-gradient layers
+    if (KS != 5 || fx != 0 || it != 4) return -4;
+    switch (epi) {
+      case EPI_BIAS: return launch_up<5, 4, EPI_BIAS, 0, true>(p, st);
+      case EPI_IGDN: return launch_up<5, 4, EPI_IGDN, 0, true>(p, st);
+      case EPI_GDN_BWD: return launch_up<5, 4, EPI_GDN_BWD, 0, true>(p, st);
+      default: return -5;
+    }
+  }
   if (KS == 5) {
     if (fx == FX_T && it == 4) {
       if (epi == EPI_GDN_BWD) return launch_up<5, 4, EPI_GDN_BWD, FX_T>(p, st);
@@ -916,6 +1111,7 @@ typedef struct ica_conv_args {
   const float* mask;
   int N, Cin, Hin, Win, Cout, Hout, Wout;
   int kind, KS, S, epi, it, fill_mode, ps;
+  int prec; /* 0 fp32 operands, 1 bf16 operands (fp32 accumulate) */
 } ica_conv_args;
 
 // Channel tile (IT = number of 32-channel MFMA row tiles per wave) the conv
@@ -940,8 +1136,21 @@ int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long 
                          int flip, int it, hipStream_t st) {
   const int IT = resolve_it(O, it);
   const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC, IT);
-  hipLaunchKernelGGL(pack_conv_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc, IT, CC,
-                     order, total, flip);
+  hipLaunchKernelGGL(pack_conv_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc,
+                     IT, CC, order, total, flip);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// bf16 fragments for prec = 1 launches: the same [cb][outer][inner][it][lane][8] order as the fp32 pack
+// with CC = 16 (lane half h holds channels 8h..8h+7 of the chunk = the bf16 MFMA k map), each element
+// rounded to nearest-even bf16.  dst holds ica_pack_conv_weight_size(O, C, KS, 16, it) bf16 values.
+int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int flip,
+                              int it, hipStream_t st) {
+  const int IT = resolve_it(O, it);
+  const long total = (long)ica_pack_conv_weight_size(O, C, KS, 16, IT);
+  hipLaunchKernelGGL(pack_conv_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
+                     reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, IT, 16, order, total, flip);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -965,6 +1174,50 @@ int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, i
                2 * Hin, 2 * Win, nullptr};
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
   hipLaunchKernelGGL(conv_up3_kernel, dim3(tiles), dim3(256), 0, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// bf16x3 GDN fragments (prec = 1): for channel tiles (a, b), k-step s, part hl (0 = hi, 1 = lo), lane l:
+// element j = part of M[a*32 + (l&31)][b*32 + 16s + 8(j>>2) + 4(l>>5) + (j&3)], the k order in which the
+// accumulator registers 8s..8s+7 of a 32x32 tile serve as the B operand.  M = gamma' or gamma'^T;
+// hi = bf16(g), lo = bf16(g - hi).  gpb holds (C/32)^2 * 2048 bf16; beta_eff as ica_pack_gdn.
+__global__ void pack_gdn_bf16_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                     __bf16* __restrict__ gp, float* __restrict__ beta_eff, int C, int transpose,
+                                     float beta_bound) {
+  const int T = C / 32;
+  const long total = (long)T * T * 2048;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const float ped = 1.4551915228366852e-11f;  // 2^-36
+  const float gbound = 3.814697265625e-06f;   // 2^-18
+  if (i < total) {
+    long t = i;
+    const int j = t % 8; t /= 8;
+    const int lane = t % 64; t /= 64;
+    const int hl = t % 2; t /= 2;
+    const int s = t % 2; t /= 2;
+    const int b = t % T; t /= T;
+    const int a = (int)t;
+    const int row = a * 32 + (lane & 31), col = b * 32 + 16 * s + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+    const int gi = transpose ? (col * C + row) : (row * C + col);
+    const float g0 = fmaxf(gamma[gi], gbound);
+    const float g = fsub_rn(fmul_rn(g0, g0), ped);
+    __bf16 hi, lo;
+    split_bf(g, hi, lo);
+    gp[i] = hl ? lo : hi;
+  }
+  if (i < C) {
+    const float bb = fmaxf(beta[i], beta_bound);
+    beta_eff[i] = fsub_rn(fmul_rn(bb, bb), ped);
+  }
+}
+
+int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* beta_eff, int C, int transpose,
+                      float beta_bound, hipStream_t st) {
+  if (C % 32 != 0) return -2;
+  const long total = (long)(C / 32) * (C / 32) * 2048;
+  hipLaunchKernelGGL(pack_gdn_bf16_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gamma, beta,
+                     reinterpret_cast<__bf16*>(gpb), beta_eff, C, transpose, beta_bound);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1003,7 +1256,8 @@ int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, in
 int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   ConvParams p{a->x,    a->y,    a->wp,   a->bias, a->gp,   a->beta, a->save_x, a->save_s, a->in_x, a->in_s,
                a->N,    a->Cin,  a->Hin,  a->Win,  a->Cout, a->Hout, a->Wout,   a->save_t, a->res,  a->mask,
-               a->fill_mode, a->ps};
+               a->fill_mode, a->ps, a->prec};
+  if (a->prec != 0 && a->prec != 1) return -4;
   const int it = resolve_it(a->Cout, a->it);
   if (a->epi >= EPI_GDN && a->epi <= EPI_IGDN_BWD && a->Cout != it * 32) return -4;
   if (a->ps && (a->Cout % 16 != 0 || !(a->epi == EPI_BIAS || a->epi == EPI_RELU || a->epi == EPI_LRELU))) return -4;
@@ -1018,3 +1272,4 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
 }
 
 }  // extern "C"
+#endif  // ICA_KERNELS_ONLY

@@ -26,11 +26,11 @@ def _P(sd, prefix, name):
 class Analysis:
     """g_a = conv(3,N)-GDN-conv(N,N)-GDN-conv(N,N)-GDN-conv(N,M), all k5 s2."""
 
-    def __init__(self, sd: dict, prefix: str = "g_a", tag: str = "g_a"):
+    def __init__(self, sd: dict, prefix: str = "g_a", tag: str = "g_a", prec: int = K.PREC_FP32):
         self.tag = tag
         self.N = _P(sd, prefix, "0.weight").shape[0]
         self.M = _P(sd, prefix, "6.weight").shape[0]
-        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "conv", 2)
+        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "conv", 2, prec)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
 
@@ -39,18 +39,19 @@ class Analysis:
         for i in range(3):
             p = self.convs[i]
             h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.gdns[i], save,
-                                    tag=f"{self.tag}.{2 * i}.fwd")
+                                    tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec)
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
-        y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.6.fwd")
+        y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.6.fwd",
+                              prec=p.fwd_prec)
         return y, saved
 
     def backward(self, gy4, saved):
         g, C = gy4, self.M
         for i in (3, 2, 1):
             g, _, _ = K.conv_up(g, C, self.convs[i].bwd, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
-                                saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad")
+                                saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec)
             C = self.N
         gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad")
         return gx
@@ -59,11 +60,11 @@ class Analysis:
 class Synthesis:
     """g_s = deconv(M,N)-IGDN-deconv(N,N)-IGDN-deconv(N,N)-IGDN-deconv(N,3), all k5 s2 op1."""
 
-    def __init__(self, sd: dict, prefix: str = "g_s", tag: str = "g_s"):
+    def __init__(self, sd: dict, prefix: str = "g_s", tag: str = "g_s", prec: int = K.PREC_FP32):
         self.tag = tag
         self.M = _P(sd, prefix, "0.weight").shape[0]
         self.N = _P(sd, prefix, "0.weight").shape[1]
-        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "deconv", 2)
+        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "deconv", 2, prec)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
 
@@ -72,7 +73,7 @@ class Synthesis:
         for i in range(3):
             p = self.convs[i]
             h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gdns[i], save,
-                                  tag=f"{self.tag}.{2 * i}.fwd")
+                                  tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec)
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
@@ -83,10 +84,10 @@ class Synthesis:
         g, C = gx4, 3
         for i in (3, 2, 1):
             g, _, _ = K.conv_down(g, C, self.convs[i].bwd, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gdns[i - 1],
-                                  saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad")
+                                  saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec)
             C = self.N
         gy, _, _ = K.conv_down(g, self.N, self.convs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS,
-                               tag=f"{self.tag}.0.dgrad")
+                               tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec)
         return gy
 
 
@@ -130,12 +131,18 @@ class HyperSynthesis:
 class CodecKernels:
     """Whole-model executor from a CompressAI-format state dict (device tensors)."""
 
-    def __init__(self, sd: dict, model: str = "hyper"):
+    def __init__(self, sd: dict, model: str = "hyper", precision: str = "fp32"):
+        """precision 'bf16': g_a / g_s run bf16-operand MFMA convs (fp32 accumulate, bf16x3 GDN normaliser;
+        BASELINE config 5); h_a / h_s and the entropy models stay fp32."""
         self.model = model
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision {precision!r}: fp32 | bf16")
+        self.precision = precision
+        prec = K.PREC_BF16 if precision == "bf16" else K.PREC_FP32
         if sd["g_a.0.weight"].device.type != "cuda":
             raise RuntimeError("CodecKernels needs the state dict on the HIP device")
-        self.ga = Analysis(sd)
-        self.gs = Synthesis(sd)
+        self.ga = Analysis(sd, prec=prec)
+        self.gs = Synthesis(sd, prec=prec)
         self.N, self.M = self.ga.N, self.ga.M
         if model == "hyper":
             self.ha = HyperAnalysis(sd)

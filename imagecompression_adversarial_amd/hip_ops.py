@@ -95,6 +95,20 @@ def pack_conv(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order
     return dst
 
 
+def pack_conv_bf16(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order: int, flip: bool = False,
+                   it: int = 0) -> torch.Tensor:
+    """bf16 fragments (prec=1 launches): the CC=16 fp32 fragment order, each element rounded to bf16."""
+    w = w.detach().contiguous()
+    _dev_check(w, "weight")
+    n = int(lib().ica_pack_conv_weight_size(O, Cc, KS, 16, it))
+    dst = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    call("ica_pack_conv_weight_bf16", ptr(w), ptr(dst), O, Cc, KS, so, sc, order, int(flip), it, stream())
+    return dst
+
+
+PREC_FP32, PREC_BF16 = 0, 1
+
+
 def conv_cc(Cin: int) -> int:
     return 4 if Cin <= 4 else 16
 
@@ -116,16 +130,23 @@ class PackedConv:
     kind 'deconv' : nn.ConvTranspose2d weight [Cin][Cout][k][k]  fwd = conv_up, dgrad = conv_down
     """
 
-    def __init__(self, weight: torch.Tensor, bias, kind: str, stride: int):
+    def __init__(self, weight: torch.Tensor, bias, kind: str, stride: int, prec: int = PREC_FP32):
+        """prec=PREC_BF16 packs the k5 s2 layers with >= 16 channels on both sides of the GEMM as bf16
+        fragments (fwd_prec / bwd_prec record what each pack is; the 3-channel ends stay fp32)."""
         self.kind = kind
+        self.fwd_prec = self.bwd_prec = PREC_FP32
         self.stride = stride
         self.KS = weight.shape[-1]
         KK = self.KS * self.KS
         if kind == "conv":
             self.Cout, self.Cin = weight.shape[0], weight.shape[1]
             # forward: o = co, c = ci
-            self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
-                                 conv_cc(self.Cin))
+            if prec == PREC_BF16 and self.KS == 5 and stride == 2 and self.Cin >= 16:
+                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN)
+                self.fwd_prec = PREC_BF16
+            else:
+                self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
+                                     conv_cc(self.Cin))
             # dgrad: k5 s2 -> conv_up (o = ci, c = co); k3 s1 -> conv_down with the taps reversed
             self.bwd = None
             if self.KS == 3 and stride == 1 and self.Cout % 16 == 0:
@@ -134,6 +155,9 @@ class PackedConv:
             elif self.KS == 5 and stride == 2 and self.Cout % 16 == 0:
                 if self.Cin == 3:   # input-gradient of the first conv: Z-gather kernel
                     self.bwd = pack_up3(weight)
+                elif prec == PREC_BF16:
+                    self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP)
+                    self.bwd_prec = PREC_BF16
                 else:
                     self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16)
         elif kind == "deconv":
@@ -141,11 +165,18 @@ class PackedConv:
             # forward (conv_up): o = co, c = ci
             if self.Cout == 3 and self.KS == 5:
                 self.fwd = pack_up3(weight)
+            elif prec == PREC_BF16 and self.KS == 5:
+                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP)
+                self.fwd_prec = PREC_BF16
             else:
                 self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16)
             # dgrad (conv_down, stride 2): o = ci, c = co
-            self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,
-                                 conv_cc(self.Cout))
+            if prec == PREC_BF16 and self.KS == 5 and stride == 2 and self.Cout >= 16:
+                self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN)
+                self.bwd_prec = PREC_BF16
+            else:
+                self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,
+                                     conv_cc(self.Cout))
         else:
             raise ValueError(kind)
         self.bias = None if bias is None else bias.detach().contiguous()
@@ -164,16 +195,34 @@ class PackedGDN:
         self.beta = torch.empty(C, device=dev)
         call("ica_pack_gdn", ptr(gamma), ptr(beta), ptr(self.gp), ptr(self.beta), C, 0, GDN_BETA_BOUND, stream())
         call("ica_pack_gdn", ptr(gamma), ptr(beta), ptr(self.gpT), ptr(self.beta), C, 1, GDN_BETA_BOUND, stream())
+        self._src = (gamma, beta)
+        self.gpb = self.gpbT = None
+
+    def bf16(self):
+        """bf16x3 hi/lo fragments of gamma' / gamma'^T for prec=1 epilogues (built once, on first use)."""
+        if self.gpb is None:
+            gamma, beta = self._src
+            T = self.C // 32
+            self.gpb = torch.empty(T * T * 2048, dtype=torch.bfloat16, device=gamma.device)
+            self.gpbT = torch.empty_like(self.gpb)
+            call("ica_pack_gdn_bf16", ptr(gamma), ptr(beta), ptr(self.gpb), ptr(self.beta), self.C, 0,
+                 GDN_BETA_BOUND, stream())
+            call("ica_pack_gdn_bf16", ptr(gamma), ptr(beta), ptr(self.gpbT), ptr(self.beta), self.C, 1,
+                 GDN_BETA_BOUND, stream())
+        return self
 
 
 # --------------------------------------------------------------------------- #
 # Convolutions
 # --------------------------------------------------------------------------- #
 def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False,
-              saved=None, out=None, tag=None, save_t=None):
+              saved=None, out=None, tag=None, save_t=None, prec=PREC_FP32):
     """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s).
-    save_t: optional nChw4c output of t = dL/dn for the GDN-bwd epilogues (GDN parameter gradients)."""
+    save_t: optional nChw4c output of t = dL/dn for the GDN-bwd epilogues (GDN parameter gradients).
+    prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex)."""
     N, _, H, W, _ = x4.shape
+    if prec == PREC_BF16:
+        return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t)
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
     Wo = (W + 2 * (KS // 2) - KS) // S + 1
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
@@ -194,9 +243,11 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
 
 
 def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
-            out=None, tag=None, save_t=None):
+            out=None, tag=None, save_t=None, prec=PREC_FP32):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
+    if prec == PREC_BF16:
+        return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t)
     Ho, Wo = 2 * H, 2 * W
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
     if Cout == 3:
@@ -222,9 +273,19 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     return y, (y if ss is not None else None), ss
 
 
+def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out, tag, save_t):
+    """conv_down / conv_up semantics (returns (y4, save_x, save_s)) for a bf16-operand launch."""
+    N, _, H, W, _ = x4.shape
+    Ho, Wo = ((H + 2 * (KS // 2) - KS) // S + 1, (W + 2 * (KS // 2) - KS) // S + 1) if kind == 0 else (2 * H, 2 * W)
+    ss = empty_nc4(N, Cout, Ho, Wo, x4.device) if (save and epi in (EPI_GDN, EPI_IGDN)) else None
+    y = conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind, epi, 0, gdn, save_s=ss, saved=saved, save_t=save_t, out=out,
+                tag=tag, prec=PREC_BF16)
+    return y, (y if ss is not None else None), ss
+
+
 def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: PackedGDN | None = None, res=None,
             save_x=None, save_s=None, saved=None, save_t=None, mask=None, fill_mode=FILL_PLAIN, ps=False,
-            out=None, tag=None, alg_rows=None):
+            out=None, tag=None, alg_rows=None, prec=PREC_FP32):
     """Generic conv launch (ica_conv_ex).  kind 0: conv2d(x, W, stride S, pad KS//2); kind 1: the stride-2
     transposed conv (dgrad of a stride-2 conv).  fill_mode 2 views x ([N, Cin/16, 2H, 2W, 4]) as the
     PixelUnshuffle(2) tensor [N, Cin/4, H, W, 4] in rho order; ps stores PixelShuffle(2) of the rho-ordered
@@ -250,10 +311,14 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
         in_x, in_s = saved
     gp = None
     if gdn is not None:
-        gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
+        if prec == PREC_BF16:
+            gdn.bf16()
+            gp = gdn.gpbT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpb
+        else:
+            gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
     a = ConvArgs(ptr(x4), ptr(y), ptr(wp), ptr(bias), ptr(gp), ptr(None if gdn is None else gdn.beta), ptr(save_x),
                  ptr(save_s), ptr(in_x), ptr(in_s), ptr(save_t), ptr(res), ptr(mask), N, Cin, H, W, Cout, Ho, Wo,
-                 kind, KS, S, epi, it, fill_mode, int(bool(ps)))
+                 kind, KS, S, epi, it, fill_mode, int(bool(ps)), int(prec))
     import ctypes
     ev = _ev_begin(tag)
     call("ica_conv_ex", ctypes.c_void_p(ctypes.addressof(a)), stream())

@@ -53,6 +53,15 @@ int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long 
  * beta_eff = max(beta, beta_bound)^2 - 2^-36.  gp holds (C/32)^2 * 1024 floats. */
 int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_eff, int C, int transpose,
                  float beta_bound, hipStream_t stream);
+/* bf16-operand packs for ica_conv_ex launches with prec = 1 (the bf16 MFMA conv path).
+ * ica_pack_conv_weight_bf16: the fragment order of ica_pack_conv_weight with CC = 16, each element rounded to
+ *   bf16 (RNE); dst holds ica_pack_conv_weight_size(O, C, KS, 16, it) bf16 values.
+ * ica_pack_gdn_bf16: gamma' (or gamma'^T) as bf16 hi/lo pairs in the k order of accumulator-as-operand MFMAs
+ *   (the GDN normaliser / GDN-bwd GEMMs run bf16x3: hi*hi + lo*hi + hi*lo); gpb holds (C/32)^2 * 2048 bf16. */
+int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order,
+                              int flip, int it, hipStream_t stream);
+int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* beta_eff, int C, int transpose,
+                      float beta_bound, hipStream_t stream);
 /* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
  * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
  * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,
@@ -94,6 +103,8 @@ typedef struct ica_conv_args {
   const float* mask;
   int N, Cin, Hin, Win, Cout, Hout, Wout;
   int kind, KS, S, epi, it, fill_mode, ps;
+  int prec; /* 0: fp32 operands (exact fp32 MFMA); 1: bf16 operands, fp32 accumulate (wp / gp from the _bf16
+             * packers; bmshj2018 k5 s2 layers: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD) */
 } ica_conv_args;
 int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);
 /* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
