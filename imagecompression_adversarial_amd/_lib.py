@@ -28,6 +28,9 @@ _SIGS = {
     "ica_pack_conv_weight_size": [_i, _i, _i, _i, _i],
     "ica_pack_conv_weight": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _i, _p],
     "ica_pack_conv_weight_bf16": [_p, _p, _i, _i, _i, _l, _l, _i, _i, _i, _p],
+    "ica_pack_conv_weight_bf16_size": [_i, _i, _i, _i],
+    "ica_pack_up3_bf16": [_p, _p, _i, _p],
+    "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_gdn_bf16": [_p, _p, _p, _p, _i, _i, _f, _p],
@@ -52,6 +55,8 @@ _SIGS = {
     "ica_eb_likelihood": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_pack_eb": [_p, _p, _p, _i, _p],
     "ica_abs": [_p, _p, _l, _p],
+    "ica_cast_f32_bf16": [_p, _p, _l, _p],
+    "ica_cast_bf16_f32": [_p, _p, _l, _p],
     "ica_round": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],
@@ -79,7 +84,7 @@ _SIGS = {
     "ica_eb_param_scatter": [_p, _p, _p, _i, _p],
     "ica_mse_grad": [_p, _p, _p, _i, _i, _i, _f, _p],
 }
-_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz}
+_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_conv_weight_bf16_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz}
 
 
 

@@ -50,25 +50,52 @@ ICA_DEV bf16x8 ld_bf8(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+ICA_DEV f32x4 bf4_to_f4(u32x2 raw) {
+  const bf16x4 b = __builtin_bit_cast(bf16x4, raw);
+  return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+}
+ICA_DEV u32x2 f4_to_bf4(f32x4 v) {
+  const bf16x4 b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  return __builtin_bit_cast(u32x2, b);
+}
+
 // Per-image view of an nChw4c tensor through a buffer descriptor (n is block-uniform): a 32-bit lane
-// offset (voff) plus a wave-uniform scalar offset (soff), so an epilogue keeps no 64-bit per-element
-// address registers live (those spilled in the GDN-backward epilogue).  One image must be < 4 GiB.
-struct Img4 {
+// offset (vq) plus a wave-uniform scalar offset (sq), both in channel quads (4 channels of one pixel:
+// 16 B fp32, 8 B when B16 = the bf16 activations of the bf16 conv path), so an epilogue keeps no 64-bit
+// per-element address registers live (those spilled in the GDN-backward epilogue).  Loads return and
+// stores take fp32 (bf16 round-to-nearest-even on store).  One image must be < 4 GiB.
+template <bool B16 = false>
+struct Img4T {
+  static constexpr unsigned ESZ = B16 ? 8u : 16u;
   __amdgpu_buffer_rsrc_t r;
-  ICA_DEV Img4(const float* base, size_t img_floats, int n)
-      : r(uniform_rsrc(base ? base + (size_t)n * img_floats : base, (unsigned)(img_floats * 4))) {}
-  ICA_DEV f32x4 ld(unsigned voff, unsigned soff) const {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+  ICA_DEV Img4T(const void* base, size_t img_quads, int n)
+      : r(uniform_rsrc(base ? static_cast<const char*>(base) + (size_t)n * img_quads * ESZ : base,
+                       (unsigned)(img_quads * ESZ))) {}
+  ICA_DEV f32x4 ld(unsigned vq, unsigned sq) const {
+    if constexpr (B16) {
+      return bf4_to_f4(__builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(vq * ESZ),
+                                                                                      (int)(sq * ESZ), 0)));
+    } else {
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(vq * ESZ), (int)(sq * ESZ), 0));
+    }
   }
-  // Stores fold the scalar offset into voff and pass a constant soffset 0.  With an SGPR soffset, hipcc
-  // (ROCm 7.2) omits the wait state between a >8-byte buffer store and a VALU overwrite of its data
-  // registers (LLVM models that hazard only for a constant soffset); on gfx950 the overwrite then
-  // corrupted dword 1 of lanes 12-15 of each 16-lane group (measured: conv_up IGDN save_s).
-  ICA_DEV void st(unsigned voff, unsigned soff, f32x4 v) const {
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(voff + soff), 0, 0);
+  // Stores fold the scalar offset into the lane offset and pass a constant soffset 0.  With an SGPR
+  // soffset, hipcc (ROCm 7.2) omits the wait state between a >8-byte buffer store and a VALU overwrite of
+  // its data registers (LLVM models that hazard only for a constant soffset); on gfx950 the overwrite
+  // then corrupted dword 1 of lanes 12-15 of each 16-lane group (measured: conv_up IGDN save_s).
+  ICA_DEV void st(unsigned vq, unsigned sq, f32x4 v) const {
+    if constexpr (B16) {
+      __builtin_amdgcn_raw_buffer_store_b64(f4_to_bf4(v), r, (int)((vq + sq) * ESZ), 0, 0);
+    } else {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)((vq + sq) * ESZ), 0, 0);
+    }
   }
 };
+typedef Img4T<false> Img4;
 ICA_DEV f32x4 bf8_as_f4(bf16x8 v) { return __builtin_bit_cast(f32x4, v); }
 ICA_DEV bf16x8 f4_as_bf8(f32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 

@@ -77,25 +77,27 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
   const int C4o = (p.Cout + 3) >> 2;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
   const unsigned pix = valid ? ((unsigned)oy * p.Wout + ox) : 0u;
-  const size_t img = (size_t)C4o * plane * 4;  // floats per image of every output-layout tensor
-  // channel group c4 = u + h (u = co_base/4 + it*8 + 2g, wave-uniform): byte offset = vo + so(u)
-  const unsigned vo = (h * plane + pix) * 16u;
-  auto so = [&](int u) -> unsigned { return (unsigned)u * plane * 16u; };
+  const size_t img = (size_t)C4o * plane;  // channel quads per image of every output-layout tensor
+  // channel group c4 = u + h (u = co_base/4 + it*8 + 2g, wave-uniform): quad offset = vo + so(u)
+  // (BF: every activation tensor of the epilogue is bf16 nChw4c, Img4T<true>)
+  using Img = Img4T<BF>;
+  const unsigned vo = h * plane + pix;
+  auto so = [&](int u) -> unsigned { return (unsigned)u * plane; };
   const int cu = co_base >> 2;
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_LRELU) {
-    const Img4 Y(p.y, img, n);
+    const Img Y(p.y, img, n);
     // PixelShuffle(2) store: output tensor [N][Cout/16][2 Hout][2 Wout][4]; rho-row quad (it, g, h) is
     // channel group c4 = (cu + it*8 + 2g) / 4 at sub-pixel q = 2(g&1) + h of the (2Hout)x(2Wout) plane
     const unsigned plane2 = 4u * plane;
-    const unsigned vo_ps = (valid ? ((unsigned)(2 * oy) * (2 * p.Wout) + 2 * ox + h) : 0u) * 16u;
+    const unsigned vo_ps = valid ? ((unsigned)(2 * oy) * (2 * p.Wout) + 2 * ox + h) : 0u;
     auto so_ps = [&](int it, int g) -> unsigned {
       const int c4 = (cu + it * 8 + 2 * g) >> 2;
-      return ((unsigned)c4 * plane2 + (unsigned)(g & 1) * (2 * p.Wout)) * 16u;
+      return (unsigned)c4 * plane2 + (unsigned)(g & 1) * (2 * p.Wout);
     };
     // (the shuffled tensor holds the same Cout * Hout * Wout floats per image as the plain one)
-    const Img4 SX((FX & FX_RES) ? p.save_x : nullptr, img, n);
-    const Img4 RS((FX & FX_RES) ? p.res : nullptr, img, n);
+    const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n);
+    const Img RS((FX & FX_RES) ? p.res : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
@@ -137,7 +139,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       }
     }
   } else if constexpr (EPI == EPI_LRELU_BWD) {
-    const Img4 Y(p.y, img, n), M(p.in_x, img, n);
+    const Img Y(p.y, img, n), M(p.in_x, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
@@ -159,8 +161,8 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // requires IT*32 == Cout, co_base == 0.  acc := x = conv + bias (kept intact
     // until every normaliser tile is done); one 32-channel tile of
     // n = beta' + gamma' x^2 at a time (16 accumulator registers live).
-    const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
-    const Img4 SX((FX & FX_RES) ? p.save_x : nullptr, img, n), RS((FX & FX_RES) ? p.res : nullptr, img, n);
+    const Img Y(p.y, img, n), SS(p.save_s, img, n);
+    const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n), RS((FX & FX_RES) ? p.res : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -242,9 +244,9 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // accumulators) and dx = g s + 2 x u with x, s re-read (L2-hot).
     // Residual gradient: added unconditionally (r = 0 without one) so that the accumulators are
     // never live in two versions across a branch (that doubled the register footprint).
-    const Img4 Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
+    const Img Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
     if constexpr ((FX & FX_RES) != 0) {
-      const Img4 SX(p.save_x, img, n), RS(p.res, img, n);
+      const Img SX(p.save_x, img, n), RS(p.res, img, n);
 #pragma unroll
       for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -275,7 +277,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       }
     }
     f32x16 tt[IT];
-    const Img4 ST((FX & FX_T) ? p.save_t : nullptr, img, n);
+    const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -395,8 +397,9 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   constexpr int WSTEP = IT * 64 * KH;  // floats per (chunk, tap)
   // bf16 operands (BF): one 16-B LDS entry holds 8 channels of a pixel as bf16 (2 entries per
   // 16-channel chunk, entry h = channels 8h..8h+7 = the B fragment of lane half h)
-  constexpr int NE = BF ? NQ / 2 : NQ;
-  static_assert(!BF || CC == 16, "bf16 conv_down needs 16-channel chunks");
+  constexpr int NE = (BF && CC == 16) ? NQ / 2 : NQ;
+  // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
+  static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
   __shared__ f32x4 patch[NE * PLANE];
 
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
@@ -453,9 +456,17 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
     for (int e = threadIdx.x; e < NE * PLANE; e += 256) {
       const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
       const int iy = iy0 + pr, ix = ix0 + pc;
-      if constexpr (BF) {
+      if constexpr (BF && CC == 16) {
+        // bf16 activations: the two channel quads are two 8-B loads, concatenated as they are
+        static_assert(!BF || FX == 0, "bf16 conv_down fill: plain view only");
         const int c4 = ch * NQ + 2 * q;
-        patch[e] = bf8_as_f4(to_bf8(ldc4(c4, iy, ix), ldc4(c4 + 1, iy, ix)));
+        u32x2 a = {0u, 0u}, b = {0u, 0u};
+        if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
+          const u32x2* xb = reinterpret_cast<const u32x2*>(p.x) + (((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix;
+          a = xb[0];
+          b = xb[(size_t)p.Hin * p.Win];
+        }
+        patch[e] = __builtin_bit_cast(f32x4, (u32x4_t){a[0], a[1], b[0], b[1]});
       } else {
         patch[e] = ldc4(ch * NQ + q, iy, ix);
       }
@@ -466,7 +477,46 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   constexpr int KK = KS * KS;
   const int total = nch * KK;
   const int lbase = (S * oyl) * PC + S * oxl;
-  if constexpr (BF) {
+  if constexpr (BF && CC == 4) {
+    // bf16, 3-channel input: k = 8h + j of tap group tg is tap 4tg + 2h + (j>>2), channel j&3, so a lane's
+    // B fragment is the f32x4 pixels of two taps (rounded to bf16); 7 MFMAs per tile cover the 25 taps
+    // (fp32 CC = 4 needs 50).  Weights: [cb][tg][it][lane][8] bf16 (pack_conv_tg_kernel), 4-set ring.
+    constexpr int TG = (KK + 3) / 4;
+    fill(0);
+    const bf16x8* wb = reinterpret_cast<const bf16x8*>(p.wp) + (size_t)cb * TG * IT * 64 + lane;
+    bf16x8 fr[4][IT];
+    auto ldw = [&](bf16x8 (&a)[IT], int g) {
+      const bf16x8* w = wb + (size_t)min(g, TG - 1) * IT * 64;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) a[it] = w[it * 64];
+    };
+    auto tapoff = [&](int t) {
+      t = min(t, KK - 1);  // taps past KK carry zero weights; read any finite patch value
+      const int ky = t / KS, kx = t - ky * KS;
+      return lbase + ky * PC + kx;
+    };
+    auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int g) {
+      ldw(nxt, g + 3);
+      const int t0 = 4 * g + 2 * h;
+      const bf16x8 b = to_bf8(patch[tapoff(t0)], patch[tapoff(t0 + 1)]);
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], b, acc[it]);
+    };
+    ldw(fr[0], 0);
+    ldw(fr[1], 1);
+    ldw(fr[2], 2);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 4 <= TG; g += 4) {
+      step(fr[0], fr[3], g);
+      step(fr[1], fr[0], g + 1);
+      step(fr[2], fr[1], g + 2);
+      step(fr[3], fr[2], g + 3);
+    }
+    if (g < TG) step(fr[0], fr[3], g);
+    if (g + 1 < TG) step(fr[1], fr[0], g + 1);
+    if (g + 2 < TG) step(fr[2], fr[1], g + 2);
+  } else if constexpr (BF) {
     // bf16: one v_mfma_f32_32x32x16_bf16 per (chunk, tap, tile) = 32 cycles, so the weight
     // fragments (16 B per lane per tile, L2-resident) are prefetched 3 steps ahead in a 4-set
     // register ring (indices compile-time via a 4x unrolled loop: no scratch, no copies).
@@ -658,17 +708,16 @@ __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
     const int q = e / UP_PLANE, rem = e - q * UP_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
     const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
     const bool ok = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const float* xp = p.x + ((((size_t)n * Cin4 + (BF ? 2 * q : q)) * p.Hin + iy) * p.Win + ix) * 4;
+    const size_t xo = (((size_t)n * Cin4 + (BF ? 2 * q : q)) * p.Hin + iy) * p.Win + ix;  // quad index
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (BF) {
-      f32x4 v1 = v;
+    if constexpr (BF) {  // bf16 activations: two 8-B channel quads per 16-B LDS entry
       if (ok) {
-        v = ld4(xp);
-        v1 = ld4(xp + (size_t)p.Hin * p.Win * 4);
+        const u32x2* xb = reinterpret_cast<const u32x2*>(p.x) + xo;
+        const u32x2 a = xb[0], b = xb[(size_t)p.Hin * p.Win];
+        v = __builtin_bit_cast(f32x4, (u32x4_t){a[0], a[1], b[0], b[1]});
       }
-      v = bf8_as_f4(to_bf8(v, v1));
     } else {
-      if (ok) v = ld4(xp);
+      if (ok) v = ld4(p.x + xo * 4);
     }
     patch[e] = v;
   }
@@ -701,6 +750,7 @@ __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
 constexpr int T3_TH = 8, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 340
 constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                            // 11
 
+template <bool BF>
 __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
   __shared__ float zs[T3_ROWS * T3_NPX];
   const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
@@ -723,46 +773,78 @@ __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
     f32x16 acc[3];
 #pragma unroll
     for (int it = 0; it < 3; ++it) acc[it] = f32x16{0};
-    const float* wl = p.wp + (size_t)lane * 8;
-    // B (activations, straight from HBM: 32 consecutive pixels x 16 B per plane = 512 B
-    // coalesced) and A (weights, L2) for chunk ch+1 are loaded while chunk ch computes.
-    auto load = [&](int ch, f32x4& v0, f32x4& v1, float (&a)[3][8]) {
-      v0 = f32x4{0.f, 0.f, 0.f, 0.f};
-      v1 = v0;
-      if (ok) {
-        v0 = ld4(xp + (size_t)(4 * ch + 2 * h) * plane * 4);
-        v1 = ld4(xp + (size_t)(4 * ch + 2 * h + 1) * plane * 4);
-      }
+    if constexpr (BF) {
+      // bf16: the 8 channels a lane loads are the k = 8h..8h+7 slice of ONE 32x32x16 MFMA per tile, so a
+      // chunk is 3 MFMAs; the B loads (HBM) and A loads (L2) of 4 chunks are issued before their MFMAs.
+      const bf16x8* wl = reinterpret_cast<const bf16x8*>(p.wp) + lane;
+      const u32x2* xq = reinterpret_cast<const u32x2*>(p.x) + (((size_t)n * Cin4) * plane + (ok ? (size_t)iy * p.Win + ix : 0));
+#pragma unroll 1
+      for (int ch0 = 0; ch0 < nch; ch0 += 4) {
+        f32x4 v0[4];
+        bf16x8 a[4][3];
 #pragma unroll
-      for (int it = 0; it < 3; ++it) {
-        const float* wt = wl + ((size_t)it * nch + ch) * 512;
-        const f32x4 w0 = ld4(wt), w1 = ld4(wt + 4);
+        for (int c = 0; c < 4; ++c) {
+          const int ch = min(ch0 + c, nch - 1);
+          u32x2 qa = {0u, 0u}, qb = {0u, 0u};   // bf16 activations: 8-B channel quads
+          if (ok) {
+            qa = xq[(size_t)(4 * ch + 2 * h) * plane];
+            qb = xq[(size_t)(4 * ch + 2 * h + 1) * plane];
+          }
+          v0[c] = __builtin_bit_cast(f32x4, (u32x4_t){qa[0], qa[1], qb[0], qb[1]});
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[it][e] = w0[e];
-          a[it][4 + e] = w1[e];
+          for (int it = 0; it < 3; ++it) a[c][it] = wl[((size_t)it * nch + ch) * 64];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (ch0 + c < nch) {
+            const bf16x8 b = f4_as_bf8(v0[c]);
+#pragma unroll
+            for (int it = 0; it < 3; ++it) acc[it] = mfma32bf(a[c][it], b, acc[it]);
+          }
         }
       }
-    };
-    auto compute = [&](const f32x4& v0, const f32x4& v1, const float (&a)[3][8]) {
-      const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    } else {
+      const float* wl = p.wp + (size_t)lane * 8;
+      // B (activations, straight from HBM: 32 consecutive pixels x 16 B per plane = 512 B
+      // coalesced) and A (weights, L2) for chunk ch+1 are loaded while chunk ch computes.
+      auto load = [&](int ch, f32x4& v0, f32x4& v1, float (&a)[3][8]) {
+        v0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        v1 = v0;
+        if (ok) {
+          v0 = ld4(xp + (size_t)(4 * ch + 2 * h) * plane * 4);
+          v1 = ld4(xp + (size_t)(4 * ch + 2 * h + 1) * plane * 4);
+        }
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2)
+        for (int it = 0; it < 3; ++it) {
+          const float* wt = wl + ((size_t)it * nch + ch) * 512;
+          const f32x4 w0 = ld4(wt), w1 = ld4(wt + 4);
 #pragma unroll
-        for (int it = 0; it < 3; ++it) acc[it] = mfma32(a[it][s2], b[s2], acc[it]);
-    };
-    f32x4 pa0, pa1, pb0, pb1;
-    float aa[3][8], ab[3][8];
-    load(0, pa0, pa1, aa);
-    int ch = 0;
+          for (int e = 0; e < 4; ++e) {
+            a[it][e] = w0[e];
+            a[it][4 + e] = w1[e];
+          }
+        }
+      };
+      auto compute = [&](const f32x4& v0, const f32x4& v1, const float (&a)[3][8]) {
+        const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+          for (int it = 0; it < 3; ++it) acc[it] = mfma32(a[it][s2], b[s2], acc[it]);
+      };
+      f32x4 pa0, pa1, pb0, pb1;
+      float aa[3][8], ab[3][8];
+      load(0, pa0, pa1, aa);
+      int ch = 0;
 #pragma unroll 1
-    for (; ch + 1 < nch; ch += 2) {
-      load(ch + 1, pb0, pb1, ab);
-      compute(pa0, pa1, aa);
-      load(min(ch + 2, nch - 1), pa0, pa1, aa);
-      compute(pb0, pb1, ab);
+      for (; ch + 1 < nch; ch += 2) {
+        load(ch + 1, pb0, pb1, ab);
+        compute(pa0, pa1, aa);
+        load(min(ch + 2, nch - 1), pa0, pa1, aa);
+        compute(pb0, pb1, ab);
+      }
+      if (ch < nch) compute(pa0, pa1, aa);
     }
-    if (ch < nch) compute(pa0, pa1, aa);
     if (q < T3_NPX) {
 #pragma unroll
       for (int it = 0; it < 3; ++it)
@@ -803,7 +885,8 @@ __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
   }
 }
 
-__global__ void pack_up3_kernel(const float* __restrict__ w, float* __restrict__ dst, int Cin, long total) {
+template <typename T>
+__global__ void pack_up3_kernel(const float* __restrict__ w, T* __restrict__ dst, int Cin, long total) {
   // w: [Cin][3][5][5] (transposed-conv view); dst[it][chunk][lane][8]
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
@@ -820,7 +903,7 @@ __global__ void pack_up3_kernel(const float* __restrict__ w, float* __restrict__
     const int co = row / 25, tap = row % 25;
     v = w[((size_t)c * 3 + co) * 25 + tap];
   }
-  dst[i] = v;
+  dst[i] = (T)v;
 }
 
 // --------------------------------------------------------------------------
@@ -944,6 +1027,11 @@ constexpr bool down_bf() {
   return KS == 5 && S == 2 && FX == 0 && (IT == 3 || IT == 4) &&
          (EPI == EPI_BIAS || EPI == EPI_GDN || EPI == EPI_IGDN_BWD);
 }
+// ... and the RGB-input ones (g_a.0 forward, g_s.6 input-gradient): 4-channel tap groups
+template <int KS, int S, int IT, int EPI, int FX>
+constexpr bool down_bf4() {
+  return KS == 5 && S == 2 && FX == 0 && IT == 4 && (EPI == EPI_GDN || EPI == EPI_IGDN_BWD);
+}
 
 template <int KS, int S, int IT, int EPI, int FX>
 static int pick_cc_down(const ConvParams& p, hipStream_t st) {
@@ -951,10 +1039,11 @@ static int pick_cc_down(const ConvParams& p, hipStream_t st) {
     return -4;
   } else {
     if (p.prec == 1) {
-      if constexpr (down_bf<KS, S, IT, EPI, FX>()) {
-        if (p.Cin <= 4) return -2;
-        return pick_tw_down<KS, S, IT, 16, EPI, FX, true>(p, st);
+      if (p.Cin <= 4) {
+        if constexpr (down_bf4<KS, S, IT, EPI, FX>()) return pick_tw_down<KS, S, IT, 4, EPI, FX, true>(p, st);
+        return -4;
       }
+      if constexpr (down_bf<KS, S, IT, EPI, FX>()) return pick_tw_down<KS, S, IT, 16, EPI, FX, true>(p, st);
       return -4;
     }
     if (p.Cin <= 4) {
@@ -1142,12 +1231,51 @@ int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long 
   return 0;
 }
 
+// bf16 tap-group fragments for a conv_down with C <= 4 input channels: [cb][tg][it][lane][8] with
+// o = cb*IT*32 + it*32 + (lane&31), tap = 4 tg + 2 (lane>>5) + (s>>2), c = s & 3 (0 past KS*KS or C).
+__global__ void pack_conv_tg_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int O, int C, int KS,
+                                    long so, long sc, int IT, long total, int flip) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int KK = KS * KS, TG = (KK + 3) / 4;
+  long t = i;
+  const int s = t % 8; t /= 8;
+  const int lane = t % 64; t /= 64;
+  const int it = t % IT; t /= IT;
+  const int tg = t % TG; t /= TG;
+  const int cb = (int)t;
+  const int o = cb * IT * 32 + it * 32 + (lane & 31);
+  const int tap = 4 * tg + 2 * (lane >> 5) + (s >> 2), c = s & 3;
+  float v = 0.f;
+  if (o < O && c < C && tap < KK) {
+    const int wt = flip ? KK - 1 - tap : tap;
+    v = w[o * so + c * sc + (wt / KS) * KS + (wt % KS)];
+  }
+  dst[i] = (__bf16)v;
+}
+
+// bf16 values ica_pack_conv_weight_bf16 writes for W[O][C][KS][KS] (C <= 4: tap groups, else CC = 16 chunks)
+size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it) {
+  if (C > 4) return ica_pack_conv_weight_size(O, C, KS, 16, it);
+  const int IT = resolve_it(O, it);
+  const int ncb = (O + IT * 32 - 1) / (IT * 32);
+  return (size_t)ncb * ((KS * KS + 3) / 4) * IT * 64 * 8;
+}
+
 // bf16 fragments for prec = 1 launches: the same [cb][outer][inner][it][lane][8] order as the fp32 pack
 // with CC = 16 (lane half h holds channels 8h..8h+7 of the chunk = the bf16 MFMA k map), each element
 // rounded to nearest-even bf16.  dst holds ica_pack_conv_weight_size(O, C, KS, 16, it) bf16 values.
 int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int flip,
                               int it, hipStream_t st) {
   const int IT = resolve_it(O, it);
+  if (C <= 4) {  // conv_down tap groups (RGB input)
+    if (order != 0) return -4;
+    const long tot = (long)ica_pack_conv_weight_bf16_size(O, C, KS, IT);
+    hipLaunchKernelGGL(pack_conv_tg_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
+                       O, C, KS, so, sc, IT, tot, flip);
+    ICA_CHECK_LAUNCH();
+    return 0;
+  }
   const long total = (long)ica_pack_conv_weight_size(O, C, KS, 16, IT);
   hipLaunchKernelGGL(pack_conv_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, IT, 16, order, total, flip);
@@ -1162,7 +1290,7 @@ size_t ica_pack_up3_size(int Cin) { return (size_t)3 * (Cin / 16) * 64 * 8; }
 int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
   const long total = (long)ica_pack_up3_size(Cin);
-  hipLaunchKernelGGL(pack_up3_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, Cin, total);
+  hipLaunchKernelGGL(pack_up3_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, Cin, total);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1173,7 +1301,28 @@ int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, i
   ConvParams p{x, y, wp, bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, Cin, Hin, Win, 3,
                2 * Hin, 2 * Win, nullptr};
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
-  hipLaunchKernelGGL(conv_up3_kernel, dim3(tiles), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(conv_up3_kernel<false>, dim3(tiles), dim3(256), 0, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// bf16-operand variants (prec = 1): fragments in the fp32 order rounded to bf16 (ica_pack_up3_size(Cin) values)
+int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t st) {
+  if (Cin % 16 != 0) return -2;
+  const long total = (long)ica_pack_up3_size(Cin);
+  hipLaunchKernelGGL(pack_up3_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
+                     reinterpret_cast<__bf16*>(dst), Cin, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                      hipStream_t st) {
+  if (Cin % 16 != 0) return -2;
+  ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+               N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
+  const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
+  hipLaunchKernelGGL(conv_up3_kernel<true>, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }

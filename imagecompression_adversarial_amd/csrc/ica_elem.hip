@@ -474,6 +474,17 @@ __global__ void abs_kernel(const float* __restrict__ x, float* __restrict__ y, l
     y[i] = fabsf(x[i]);
 }
 
+// fp32 <-> bf16 activation casts at the ends of the bf16 conv path (latent for the entropy models,
+// y_hat into g_s): 4 values per thread, RNE (v_cvt_pk_bf16_f32) / exact widening.
+__global__ void cast_f32_bf16_kernel(const f32x4* __restrict__ x, u32x2* __restrict__ y, long nq) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (long)gridDim.x * blockDim.x)
+    y[i] = f4_to_bf4(x[i]);
+}
+__global__ void cast_bf16_f32_kernel(const u32x2* __restrict__ x, f32x4* __restrict__ y, long nq) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (long)gridDim.x * blockDim.x)
+    y[i] = bf4_to_f4(x[i]);
+}
+
 // round half to even (torch.round / quantize "dequantize" with means=None; SURVEY §8 a16: rintf)
 __global__ void round_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -665,6 +676,23 @@ int ica_pack_eb(const float* const* params, float* prm, float* med, int C, hipSt
 
 int ica_round(const float* x, float* y, long n, hipStream_t st) {
   hipLaunchKernelGGL(round_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// n must be a multiple of 4 (nChw4c tensors)
+int ica_cast_f32_bf16(const float* x, void* y, long n, hipStream_t st) {
+  if (n % 4) return -2;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_1d(n / 4)), dim3(256), 0, st, reinterpret_cast<const f32x4*>(x),
+                     reinterpret_cast<u32x2*>(y), n / 4);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_cast_bf16_f32(const void* x, float* y, long n, hipStream_t st) {
+  if (n % 4) return -2;
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_1d(n / 4)), dim3(256), 0, st, reinterpret_cast<const u32x2*>(x),
+                     reinterpret_cast<f32x4*>(y), n / 4);
   ICA_CHECK_LAUNCH();
   return 0;
 }

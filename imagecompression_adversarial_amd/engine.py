@@ -16,6 +16,8 @@ gradients).
 """
 from __future__ import annotations
 
+import torch
+
 from . import hip_ops as K
 
 
@@ -53,7 +55,8 @@ class Analysis:
             g, _, _ = K.conv_up(g, C, self.convs[i].bwd, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
                                 saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec)
             C = self.N
-        gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad")
+        gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad",
+                             prec=self.convs[0].bwd_prec)
         return gx
 
 
@@ -77,7 +80,7 @@ class Synthesis:
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
-        xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS, tag=f"{self.tag}.6.fwd")
+        xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS, tag=f"{self.tag}.6.fwd", prec=p.fwd_prec)
         return xh, saved
 
     def backward(self, gx4, saved):
@@ -162,17 +165,23 @@ class CodecKernels:
     def g_s_backward(self, gx4, saved):
         return self.gs.backward(gx4, saved)
 
+    def _to_gs(self, yh4):
+        """y_hat into g_s: bf16 activations on the bf16 path (rounded latents are exact in bf16 up to 256)."""
+        return K.cast_nc4(yh4, torch.bfloat16) if self.precision == "bf16" else yh4
+
     def forward(self, x4, training=False, noise_y4=None, noise_z4=None):
         """net(x) (anchors/balle.py:25-55): x_hat4, y4, likelihood tensors and per-image sum log p."""
         y4, _ = self.ga.forward(x4)
+        if self.precision == "bf16":   # the entropy models and h_a run fp32
+            y4 = K.cast_nc4(y4, torch.float32)
         if self.model == "factorized":
             yh, ylik, ysum = K.eb_likelihood(y4, self.M, self.eb, training, noise_y4)
-            xh, _ = self.gs.forward(yh)
+            xh, _ = self.gs.forward(self._to_gs(yh))
             return {"x_hat4": xh, "y4": y4, "y_hat4": yh, "lik4": {"y": ylik}, "sumlog": ysum}
         z4 = self.ha.forward(y4)
         zh, zlik, zsum = K.eb_likelihood(z4, self.N, self.eb, training, noise_z4)
         s4 = self.hs.forward(zh)
         yh, ylik, ysum = K.gc_likelihood(y4, self.M, s4, None, training, noise_y4)
-        xh, _ = self.gs.forward(yh)
+        xh, _ = self.gs.forward(self._to_gs(yh))
         return {"x_hat4": xh, "y4": y4, "y_hat4": yh, "z4": z4, "z_hat4": zh, "scales4": s4,
                 "lik4": {"y": ylik, "z": zlik}, "sumlog": ysum + zsum}

@@ -59,8 +59,24 @@ def c4(C: int) -> int:
     return (C + 3) // 4
 
 
-def empty_nc4(N, C, H, W, device):
-    return torch.empty((N, c4(C), H, W, 4), dtype=torch.float32, device=device)
+def empty_nc4(N, C, H, W, device, dtype=torch.float32):
+    return torch.empty((N, c4(C), H, W, 4), dtype=dtype, device=device)
+
+
+def cast_nc4(x4: torch.Tensor, dtype) -> torch.Tensor:
+    """fp32 <-> bf16 copy of an nChw4c tensor (the ends of the bf16 conv path) on the HIP cast kernels."""
+    if x4.dtype == dtype:
+        return x4
+    if not x4.is_cuda or not x4.is_contiguous():
+        raise RuntimeError("cast_nc4 needs a contiguous HIP tensor")
+    y = torch.empty(x4.shape, dtype=dtype, device=x4.device)
+    if dtype == torch.bfloat16 and x4.dtype == torch.float32:
+        call("ica_cast_f32_bf16", ptr(x4), ptr(y), x4.numel(), stream())
+    elif dtype == torch.float32 and x4.dtype == torch.bfloat16:
+        call("ica_cast_bf16_f32", ptr(x4), ptr(y), x4.numel(), stream())
+    else:
+        raise RuntimeError(f"cast_nc4 {x4.dtype} -> {dtype}")
+    return y
 
 
 def to_nc4(x: torch.Tensor) -> torch.Tensor:
@@ -100,7 +116,7 @@ def pack_conv_bf16(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, 
     """bf16 fragments (prec=1 launches): the CC=16 fp32 fragment order, each element rounded to bf16."""
     w = w.detach().contiguous()
     _dev_check(w, "weight")
-    n = int(lib().ica_pack_conv_weight_size(O, Cc, KS, 16, it))
+    n = int(lib().ica_pack_conv_weight_bf16_size(O, Cc, KS, it))
     dst = torch.empty(n, dtype=torch.bfloat16, device=w.device)
     call("ica_pack_conv_weight_bf16", ptr(w), ptr(dst), O, Cc, KS, so, sc, order, int(flip), it, stream())
     return dst
@@ -113,13 +129,18 @@ def conv_cc(Cin: int) -> int:
     return 4 if Cin <= 4 else 16
 
 
-def pack_up3(w_view: torch.Tensor) -> torch.Tensor:
-    """Fragments for conv_up3 from a [Cin][3][5][5] transposed-conv weight view."""
+def pack_up3(w_view: torch.Tensor, prec: int = 0) -> torch.Tensor:
+    """Fragments for conv_up3 from a [Cin][3][5][5] transposed-conv weight view (prec 1: bf16)."""
     w = w_view.detach().contiguous()
     _dev_check(w, "weight")
     Cin = w.shape[0]
-    dst = torch.empty(int(lib().ica_pack_up3_size(Cin)), device=w.device)
-    call("ica_pack_up3", ptr(w), ptr(dst), Cin, stream())
+    n = int(lib().ica_pack_up3_size(Cin))
+    if prec:
+        dst = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+        call("ica_pack_up3_bf16", ptr(w), ptr(dst), Cin, stream())
+    else:
+        dst = torch.empty(n, device=w.device)
+        call("ica_pack_up3", ptr(w), ptr(dst), Cin, stream())
     return dst
 
 
@@ -131,8 +152,8 @@ class PackedConv:
     """
 
     def __init__(self, weight: torch.Tensor, bias, kind: str, stride: int, prec: int = PREC_FP32):
-        """prec=PREC_BF16 packs the k5 s2 layers with >= 16 channels on both sides of the GEMM as bf16
-        fragments (fwd_prec / bwd_prec record what each pack is; the 3-channel ends stay fp32)."""
+        """prec=PREC_BF16 packs the k5 s2 layers as bf16 fragments (fwd_prec / bwd_prec record what each pack
+        is): 16-channel chunks, 4-tap groups for an RGB conv input, the Z-gather pack for 3-channel outputs."""
         self.kind = kind
         self.fwd_prec = self.bwd_prec = PREC_FP32
         self.stride = stride
@@ -141,7 +162,7 @@ class PackedConv:
         if kind == "conv":
             self.Cout, self.Cin = weight.shape[0], weight.shape[1]
             # forward: o = co, c = ci
-            if prec == PREC_BF16 and self.KS == 5 and stride == 2 and self.Cin >= 16:
+            if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cin >= 16 or self.Cin <= 4):
                 self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN)
                 self.fwd_prec = PREC_BF16
             else:
@@ -154,7 +175,8 @@ class PackedConv:
                                      conv_cc(self.Cout), flip=True)
             elif self.KS == 5 and stride == 2 and self.Cout % 16 == 0:
                 if self.Cin == 3:   # input-gradient of the first conv: Z-gather kernel
-                    self.bwd = pack_up3(weight)
+                    self.bwd = pack_up3(weight, prec)
+                    self.bwd_prec = prec
                 elif prec == PREC_BF16:
                     self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP)
                     self.bwd_prec = PREC_BF16
@@ -164,14 +186,15 @@ class PackedConv:
             self.Cin, self.Cout = weight.shape[0], weight.shape[1]
             # forward (conv_up): o = co, c = ci
             if self.Cout == 3 and self.KS == 5:
-                self.fwd = pack_up3(weight)
+                self.fwd = pack_up3(weight, prec)
+                self.fwd_prec = prec
             elif prec == PREC_BF16 and self.KS == 5:
                 self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP)
                 self.fwd_prec = PREC_BF16
             else:
                 self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16)
             # dgrad (conv_down, stride 2): o = ci, c = co
-            if prec == PREC_BF16 and self.KS == 5 and stride == 2 and self.Cout >= 16:
+            if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cout >= 16 or self.Cout <= 4):
                 self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN)
                 self.bwd_prec = PREC_BF16
             else:
@@ -246,7 +269,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
             out=None, tag=None, save_t=None, prec=PREC_FP32):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
-    if prec == PREC_BF16:
+    if prec == PREC_BF16 and Cout != 3:
         return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t)
     Ho, Wo = 2 * H, 2 * W
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
@@ -254,7 +277,8 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
         if epi != EPI_BIAS:
             raise RuntimeError("conv_up to 3 channels supports the bias epilogue only")
         ev = _ev_begin(tag)
-        call("ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, stream())
+        call("ica_conv_up3_bf16" if prec == PREC_BF16 else "ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
+             Cin, H, W, stream())
         _ev_end(ev)
         return y, None, None
     ss = None
@@ -277,7 +301,7 @@ def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out,
     """conv_down / conv_up semantics (returns (y4, save_x, save_s)) for a bf16-operand launch."""
     N, _, H, W, _ = x4.shape
     Ho, Wo = ((H + 2 * (KS // 2) - KS) // S + 1, (W + 2 * (KS // 2) - KS) // S + 1) if kind == 0 else (2 * H, 2 * W)
-    ss = empty_nc4(N, Cout, Ho, Wo, x4.device) if (save and epi in (EPI_GDN, EPI_IGDN)) else None
+    ss = empty_nc4(N, Cout, Ho, Wo, x4.device, torch.bfloat16) if (save and epi in (EPI_GDN, EPI_IGDN)) else None
     y = conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind, epi, 0, gdn, save_s=ss, saved=saved, save_t=save_t, out=out,
                 tag=tag, prec=PREC_BF16)
     return y, (y if ss is not None else None), ss
@@ -300,12 +324,13 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
         Wo = (W + 2 * (KS // 2) - KS) // S + 1
     else:
         Ho, Wo = 2 * H, 2 * W
+    dt = torch.bfloat16 if prec == PREC_BF16 else torch.float32   # bf16 path: bf16 activations
     if out is not None:
         y = out
     elif ps:
-        y = torch.empty((N, Cout // 16, 2 * Ho, 2 * Wo, 4), dtype=torch.float32, device=x4.device)
+        y = torch.empty((N, Cout // 16, 2 * Ho, 2 * Wo, 4), dtype=dt, device=x4.device)
     else:
-        y = empty_nc4(N, Cout, Ho, Wo, x4.device)
+        y = empty_nc4(N, Cout, Ho, Wo, x4.device, dt)
     in_x = in_s = None
     if saved is not None:
         in_x, in_s = saved

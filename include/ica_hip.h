@@ -62,6 +62,18 @@ int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, l
                               int flip, int it, hipStream_t stream);
 int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* beta_eff, int C, int transpose,
                       float beta_bound, hipStream_t stream);
+/* bf16 values ica_pack_conv_weight_bf16 writes.  C <= 4 (an RGB conv input; conv_down only) packs "tap groups":
+ * k = 8h + j of MFMA tg is tap 4tg + 2h + (j>>2), channel j&3 (7 MFMAs per 32-row tile for 5x5 taps). */
+size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it);
+/* bf16 Z-gather transposed conv to 3 channels (g_s last layer / g_a first-layer input-gradient). */
+int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t stream);
+int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                      hipStream_t stream);
+/* bf16 conv path activations are bf16 nChw4c (8 B per channel quad): every prec = 1 conv_down / conv_up reads
+ * bf16 x (except 4-channel RGB inputs, fp32), writes bf16 y / save_s and reads bf16 in_x / in_s; the Z-gather
+ * kernel reads bf16 x and writes fp32 y.  Casts for the tensors that leave the path (n % 4 == 0): */
+int ica_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
+int ica_cast_bf16_f32(const void* x, float* y, long n, hipStream_t stream);
 /* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
  * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
  * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,

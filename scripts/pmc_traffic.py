@@ -1,13 +1,13 @@
-"""HBM traffic per launch of the hyper bench's tagged kernels, from rocprofv3 --pmc passes
+"""HBM traffic per launch of the bench's tagged g_a / g_s kernels, from rocprofv3 --pmc passes
 (FETCH_SIZE pass and WRITE_SIZE pass, run separately: scripts/gpu_pmc.sh).
 
 Correction (MI355X_MICROARCH.md, "HBM [CDNA4]"): on gfx950 FETCH_SIZE reports half the bytes of wide
 coalesced streaming reads, so bytes_read = 2 * FETCH_SIZE (KB); WRITE_SIZE is exact for 16-B/lane stores.
 Our loads/stores are 16 B per lane (nChw4c float4), so both corrections apply as stated.
 
-Kernels are identified by (name prefix, Grid_Size) for the bench configuration (hyper q3, 32 x 512x768);
-the grids follow the launchers in ica_conv.hip.  Writes profiles/pmc_traffic.json {tag: bytes/launch}.
-    python scripts/pmc_traffic.py gpurun_out/pmc > profiles/pmc_traffic.json
+Kernels are identified by (name prefix, Grid_Size); the grids follow the launchers in ica_conv.hip.
+    python scripts/pmc_traffic.py gpurun_out/pmc [B H W prec] > profiles/pmc_traffic.json
+(default: config 2 = 32 x 512x768 fp32; config 5 = 8 2048 2048 bf16).  Output {tag: bytes/launch}.
 """
 import collections
 import csv
@@ -16,41 +16,41 @@ import json
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-B = 32
+B, H, W = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (32, 512, 768)
+PREC = sys.argv[5] if len(sys.argv) > 5 else "fp32"
+BF = "true" if PREC == "bf16" else "false"
 TH = {32: 4, 16: 8}
 
 
-def down_grid(Hout, Wout, Cout, it, tw):
-    tiles = -(-Wout // tw) * -(-Hout // TH[tw]) * B
-    return tiles * 256 * -(-Cout // (it * 32))
+def tw(Wout):
+    return 32 if Wout >= 32 and Wout % 32 == 0 else 16
 
 
-def up_grid(Hin, Win, Cout, it):
-    return -(-Win // 16) * -(-Hin // 4) * B * 256 * -(-Cout // (it * 32))
+def down(cc, epi, Hout, Wout, Cout, it):
+    t = tw(Wout)
+    grid = -(-Wout // t) * -(-Hout // TH[t]) * B * 256 * -(-Cout // (it * 32))
+    return f"void conv_down_kernel<5, 2, {it}, {cc}, {t}, {epi}, 0, {BF}>", grid
 
 
-def up3_grid(Hin, Win):
-    return -(-Win // 32) * -(-Hin // 8) * B * 256
+def up(epi, Hin, Win, Cout, it):
+    return f"void conv_up_kernel<5, {it}, {epi}, 0, {BF}>", -(-Win // 16) * -(-Hin // 4) * B * 256 * -(-Cout // (it * 32))
 
 
-# tag -> (kernel-name prefix, Grid_Size)
-TAGS = {
-    "g_a.0.fwd": ("void conv_down_kernel<5, 2, 4, 4, 32, 2, 0>", down_grid(256, 384, 128, 4, 32)),
-    "g_a.2.fwd": ("void conv_down_kernel<5, 2, 4, 16, 32, 2, 0>", down_grid(128, 192, 128, 4, 32)),
-    "g_a.4.fwd": ("void conv_down_kernel<5, 2, 4, 16, 32, 2, 0>", down_grid(64, 96, 128, 4, 32)),
-    "g_a.6.fwd": ("void conv_down_kernel<5, 2, 3, 16, 16, 0, 0>", down_grid(32, 48, 192, 3, 16)),
-    "g_s.0.fwd": ("void conv_up_kernel<5, 4, 3, 0>", up_grid(32, 48, 128, 4)),
-    "g_s.2.fwd": ("void conv_up_kernel<5, 4, 3, 0>", up_grid(64, 96, 128, 4)),
-    "g_s.4.fwd": ("void conv_up_kernel<5, 4, 3, 0>", up_grid(128, 192, 128, 4)),
-    "g_s.6.fwd": ("conv_up3_kernel", up3_grid(256, 384)),       # shares its grid with g_a.0.dgrad
-    "g_s.6.dgrad": ("void conv_down_kernel<5, 2, 4, 4, 32, 5, 0>", down_grid(256, 384, 128, 4, 32)),
-    "g_s.4.dgrad": ("void conv_down_kernel<5, 2, 4, 16, 32, 5, 0>", down_grid(128, 192, 128, 4, 32)),
-    "g_s.2.dgrad": ("void conv_down_kernel<5, 2, 4, 16, 32, 5, 0>", down_grid(64, 96, 128, 4, 32)),
-    "g_s.0.dgrad": ("void conv_down_kernel<5, 2, 3, 16, 16, 0, 0>", down_grid(32, 48, 192, 3, 16)),
-    "g_a.6.dgrad": ("void conv_up_kernel<5, 4, 4, 0>", up_grid(32, 48, 128, 4)),
-    "g_a.4.dgrad": ("void conv_up_kernel<5, 4, 4, 0>", up_grid(64, 96, 128, 4)),
-    "g_a.2.dgrad": ("void conv_up_kernel<5, 4, 4, 0>", up_grid(128, 192, 128, 4)),
-    "g_a.0.dgrad": ("conv_up3_kernel", up3_grid(256, 384)),
+def up3(Hin, Win):
+    return f"void conv_up3_kernel<{BF}>", -(-Win // 32) * -(-Hin // 8) * B * 256
+
+
+N, M = 128, 192
+h = [(H >> k, W >> k) for k in range(5)]   # resolution of level k
+TAGS = {   # epilogue ids: 0 BIAS, 2 GDN, 3 IGDN, 4 GDN_BWD, 5 IGDN_BWD
+    "g_a.0.fwd": down(4, 2, *h[1], N, 4), "g_a.2.fwd": down(16, 2, *h[2], N, 4),
+    "g_a.4.fwd": down(16, 2, *h[3], N, 4), "g_a.6.fwd": down(16, 0, *h[4], M, 3),
+    "g_s.0.fwd": up(3, *h[4], N, 4), "g_s.2.fwd": up(3, *h[3], N, 4), "g_s.4.fwd": up(3, *h[2], N, 4),
+    "g_s.6.fwd": up3(*h[1]),    # shares its name and grid with g_a.0.dgrad
+    "g_s.6.dgrad": down(4, 5, *h[1], N, 4), "g_s.4.dgrad": down(16, 5, *h[2], N, 4),
+    "g_s.2.dgrad": down(16, 5, *h[3], N, 4), "g_s.0.dgrad": down(16, 0, *h[4], M, 3),
+    "g_a.6.dgrad": up(4, *h[4], N, 4), "g_a.4.dgrad": up(4, *h[3], N, 4), "g_a.2.dgrad": up(4, *h[2], N, 4),
+    "g_a.0.dgrad": up3(*h[1]),
 }
 
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -75,6 +75,7 @@ for tag, (prefix, grid) in TAGS.items():
     out[tag] = rd + wr
     detail[tag] = {"read_bytes": rd, "write_bytes": wr}
 json.dump({**{k: round(v) for k, v in out.items()}, "_detail": detail,
-           "_note": "bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB*1024), gfx950 correction per "
-                    "MI355X_MICROARCH.md HBM section; hyper q3, 32 x 512x768"}, sys.stdout, indent=1)
+           "_note": f"bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB*1024), gfx950 correction per "
+                    f"MI355X_MICROARCH.md HBM section; hyper q3, {B} x {H}x{W}, {PREC} conv operands"},
+          sys.stdout, indent=1)
 print()

@@ -1,11 +1,13 @@
 """GPU parity of the bf16-operand conv path (BASELINE config 5).
 
-Two references per kernel:
+The bf16 path computes with bf16 conv operands (fp32 accumulate) and keeps its inter-layer activations,
+saved GDN tensors and gradients as bf16 nChw4c (the image-domain ends stay fp32).  Two references:
   * "emulated bf16": the CPU oracle's fp32 conv applied to bf16-rounded operands (x.bfloat16().float(),
-    w.bfloat16().float()).  The HIP kernel must match it to fp32 accumulation-order noise:
-    rel-max <= 2e-5 (plain convs) / 1e-4 (GDN epilogues, whose normaliser GEMM runs bf16x3 = 2^-16).
-  * the fp32 oracle itself: rel-max <= 1e-2 per layer, <= 3e-2 through the g_a+g_s chain and its input
-    gradient (the bf16 rounding of every conv operand; stated tolerance of the bf16 path).
+    w.bfloat16().float()).  fp32 outputs match it to accumulation-order noise (rel-max <= 2e-5); bf16 outputs
+    to their final rounding (<= 4e-3: half a bf16 ulp of the largest element plus noise).
+  * the fp32 oracle itself: rel-max <= 1e-2 per layer; GDN-backward epilogues (x = y/s and s read back
+    as bf16) <= 1.5e-2; <= 3e-2 through the g_a+g_s chain and its input gradient (stated tolerance of the
+    bf16 path).
 The ROI attack at the config-5 tile size (2048x2048) is checked by size-independent properties against the
 fp32 HIP path: L-inf box and [0,1] exact, reconstruction within 3e-2, same first-step branch.
 """
@@ -29,6 +31,16 @@ def bf(t):
     return t.bfloat16().float()
 
 
+def nc4b(K, x):
+    """CPU NCHW -> device bf16 nChw4c (the bf16 path's activation format)."""
+    return K.to_nc4(x.to(DEV)).bfloat16()
+
+
+def unb(K, y4, C):
+    """device nChw4c (bf16 or fp32) -> CPU NCHW fp32."""
+    return K.from_nc4(y4.float(), C).cpu()
+
+
 @pytest.fixture(scope="module")
 def K():
     from imagecompression_adversarial_amd import hip_ops
@@ -46,9 +58,10 @@ def test_conv_down_bf16(K, cin, cout, hw):
     ref = F.conv2d(x, w, b, stride=2, padding=2)
     p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2, K.PREC_BF16)
     assert p.fwd_prec == K.PREC_BF16 and p.fwd.dtype == torch.bfloat16
-    y4, _, _ = K.conv_down(K.to_nc4(x.to(DEV)), cin, p.fwd, p.bias, cout, 5, 2, K.EPI_BIAS, prec=p.fwd_prec)
-    y = K.from_nc4(y4, cout).cpu()
-    assert rel_err(y, emu) < 2e-5
+    y4, _, _ = K.conv_down(nc4b(K, x), cin, p.fwd, p.bias, cout, 5, 2, K.EPI_BIAS, prec=p.fwd_prec)
+    assert y4.dtype == torch.bfloat16
+    y = unb(K, y4, cout)
+    assert rel_err(y, emu) < 4e-3
     assert rel_err(y, ref) < 1e-2
 
 
@@ -61,9 +74,8 @@ def test_conv_up_bf16(K, cin, cout, hw):
     emu = F.conv_transpose2d(bf(x), bf(w), b, stride=2, padding=2, output_padding=1)
     p = K.PackedConv(w.to(DEV), b.to(DEV), "deconv", 2, K.PREC_BF16)
     assert p.fwd_prec == K.PREC_BF16
-    y4, _, _ = K.conv_up(K.to_nc4(x.to(DEV)), cin, p.fwd, p.bias, cout, prec=p.fwd_prec)
-    y = K.from_nc4(y4, cout).cpu()
-    assert rel_err(y, emu) < 2e-5
+    y4, _, _ = K.conv_up(nc4b(K, x), cin, p.fwd, p.bias, cout, prec=p.fwd_prec)
+    assert rel_err(unb(K, y4, cout), emu) < 4e-3
 
 
 def _gdn_params(C, seed):
@@ -83,19 +95,18 @@ def test_gdn_fwd_epilogues_bf16(K, inverse):
     b = rnd((C,), 15) * 0.1
     if not inverse:
         p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2, K.PREC_BF16)
-        y4, _, ss = K.conv_down(K.to_nc4(x.to(DEV)), C, p.fwd, p.bias, C, 5, 2, K.EPI_GDN, gdn, True,
-                                prec=p.fwd_prec)
+        y4, _, ss = K.conv_down(nc4b(K, x), C, p.fwd, p.bias, C, 5, 2, K.EPI_GDN, gdn, True, prec=p.fwd_prec)
         pre = F.conv2d(bf(x), bf(w), b, stride=2, padding=2)
     else:
         p = K.PackedConv(w.to(DEV), b.to(DEV), "deconv", 2, K.PREC_BF16)
-        y4, _, ss = K.conv_up(K.to_nc4(x.to(DEV)), C, p.fwd, p.bias, C, K.EPI_IGDN, gdn, True, prec=p.fwd_prec)
+        y4, _, ss = K.conv_up(nc4b(K, x), C, p.fwd, p.bias, C, K.EPI_IGDN, gdn, True, prec=p.fwd_prec)
         pre = F.conv_transpose2d(bf(x), bf(w), b, stride=2, padding=2, output_padding=1)
     out = codec.gdn(pre, beta, gamma, inverse)
-    assert rel_err(K.from_nc4(y4, C).cpu(), out) < 1e-4
+    assert rel_err(unb(K, y4, C), out) < 4e-3
     be, ge = codec.gdn_effective(beta, gamma)
     norm = F.conv2d(pre ** 2, ge.reshape(C, C, 1, 1), be)
     s_ref = torch.sqrt(norm) if inverse else torch.rsqrt(norm)
-    assert rel_err(K.from_nc4(ss, C).cpu(), s_ref) < 1e-4
+    assert rel_err(unb(K, ss, C), s_ref) < 4e-3
 
 
 @pytest.mark.parametrize("inverse", [False, True])
@@ -121,15 +132,14 @@ def test_gdn_bwd_epilogues_bf16(K, inverse):
     yprev = codec.gdn(ad, beta, gamma, inverse)
     s = (yprev / a).detach()
     yprev.backward(gy)
-    saved = (K.to_nc4(yprev.detach().to(DEV)), K.to_nc4(s.to(DEV)))
+    saved = (nc4b(K, yprev.detach()), nc4b(K, s))
     assert p.bwd_prec == K.PREC_BF16
     if not inverse:
-        out4, _, _ = K.conv_up(K.to_nc4(g.to(DEV)), C, p.bwd, None, C, K.EPI_GDN_BWD, gdn, saved=saved,
-                               prec=p.bwd_prec)
+        out4, _, _ = K.conv_up(nc4b(K, g), C, p.bwd, None, C, K.EPI_GDN_BWD, gdn, saved=saved, prec=p.bwd_prec)
     else:
-        out4, _, _ = K.conv_down(K.to_nc4(g.to(DEV)), C, p.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gdn, saved=saved,
+        out4, _, _ = K.conv_down(nc4b(K, g), C, p.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gdn, saved=saved,
                                  prec=p.bwd_prec)
-    assert rel_err(K.from_nc4(out4, C).cpu(), ad.grad) < 1e-4
+    assert rel_err(unb(K, out4, C), ad.grad) < 1.5e-2
 
 
 def test_chain_bf16_vs_fp32(K):
@@ -145,13 +155,14 @@ def test_chain_bf16_vs_fp32(K):
     (out_ref * gout).sum().backward()
     y4, sa = kern.g_a(K.to_nc4(x.to(DEV)), save=True)
     xh4, ss = kern.g_s(y4, save=True)
+    assert xh4.dtype == torch.float32 and y4.dtype == torch.bfloat16
     xh = K.from_nc4(xh4, 3).cpu()
     assert rel_err(xh, out_ref.detach()) < 3e-2
     g4 = K.to_nc4(gout.to(DEV))
     gx4 = kern.g_a_backward(kern.g_s_backward(g4, ss), sa)
     gx = K.from_nc4(gx4, 3).cpu()
     assert rel_err(gx, xr.grad) < 3e-2
-    assert rel_err(K.from_nc4(y4, 192).cpu(), y_ref.detach()) < 3e-2
+    assert rel_err(unb(K, y4, 192), y_ref.detach()) < 3e-2
 
 
 @pytest.mark.parametrize("roi", [(256, 1536, 512, 1792)])
@@ -176,3 +187,63 @@ def test_roi_attack_2048_bf16_properties(roi):
     assert rel_err(r16.output_s.cpu(), r32.output_s.cpu()) < 3e-2
     assert rel_err(r16.output_t.cpu(), r32.output_t.cpu()) < 3e-2
     assert [bool(v) for v in r16.branches[0]] == [bool(v) for v in r32.branches[0]]
+
+
+@pytest.mark.parametrize("hw", [(64, 96), (20, 36)])
+def test_rgb_input_conv_bf16_tap_groups(K, hw):
+    """g_a.0 forward (conv 3->128 + GDN) on bf16 4-tap x 4-channel groups vs emulated bf16."""
+    H, W = hw
+    C = 128
+    x = rnd((2, 3, H, W), 41, 0.0, 1.0)
+    w = rnd((C, 3, 5, 5), 42) * 0.1
+    b = rnd((C,), 43) * 0.1
+    beta, gamma = _gdn_params(C, 44)
+    gdn = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2, K.PREC_BF16)
+    assert p.fwd_prec == K.PREC_BF16
+    y4, _, _ = K.conv_down(K.to_nc4(x.to(DEV)), 3, p.fwd, p.bias, C, 5, 2, K.EPI_GDN, gdn, True, prec=p.fwd_prec)
+    ref = codec.gdn(F.conv2d(bf(x), bf(w), b, stride=2, padding=2), beta, gamma, False)
+    assert rel_err(unb(K, y4, C), ref) < 4e-3
+
+
+@pytest.mark.parametrize("hw", [(16, 24), (9, 13)])
+def test_rgb_output_deconv_bf16(K, hw):
+    """g_s.6 forward (deconv 128->3, Z-gather kernel) and its input-gradient (conv_down 3->128 on tap groups,
+    IGDN_BWD epilogue) on bf16 operands vs emulated bf16."""
+    H, W = hw
+    C = 128
+    x = rnd((2, C, H, W), 51)
+    w = rnd((C, 3, 5, 5), 52) * (1.0 / (3 * 25) ** 0.5)
+    b = rnd((3,), 53) * 0.1
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "deconv", 2, K.PREC_BF16)
+    assert p.fwd_prec == K.PREC_BF16 and p.bwd_prec == K.PREC_BF16
+    y4, _, _ = K.conv_up(nc4b(K, x), C, p.fwd, p.bias, 3, prec=p.fwd_prec)
+    emu = F.conv_transpose2d(bf(x), bf(w), b, stride=2, padding=2, output_padding=1)
+    assert rel_err(K.from_nc4(y4, 3).cpu(), emu) < 2e-5
+    # input-gradient through the preceding IGDN
+    beta, gamma = _gdn_params(C, 54)
+    gdn = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
+    a = rnd((1, C, H, W), 55)
+    g = rnd((1, 3, 2 * H, 2 * W), 56)
+    ad = a.clone().requires_grad_(True)
+    yprev = codec.gdn(ad, beta, gamma, True)
+    s = (yprev / a).detach()
+    yprev.backward(F.conv2d(bf(g), bf(w), None, stride=2, padding=2))
+    saved = (nc4b(K, yprev.detach()), nc4b(K, s))
+    out4, _, _ = K.conv_down(K.to_nc4(g.to(DEV)), 3, p.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gdn, saved=saved,
+                             prec=p.bwd_prec)
+    assert rel_err(unb(K, out4, C), ad.grad) < 1.5e-2
+
+
+@pytest.mark.parametrize("hw", [(32, 48), (18, 26)])
+def test_first_conv_dgrad_bf16(K, hw):
+    """g_a.0 input-gradient (Z-gather transposed conv 128->3) on bf16 operands vs emulated bf16."""
+    H, W = hw
+    C = 128
+    w = rnd((C, 3, 5, 5), 61) * 0.1
+    g = rnd((2, C, H, W), 62)
+    p = K.PackedConv(w.to(DEV), None, "conv", 2, K.PREC_BF16)
+    assert p.bwd_prec == K.PREC_BF16
+    out4, _, _ = K.conv_up(nc4b(K, g), C, p.bwd, None, 3, prec=p.bwd_prec)
+    emu = F.conv_transpose2d(bf(g), bf(w), None, stride=2, padding=2, output_padding=1)
+    assert rel_err(K.from_nc4(out4, 3).cpu(), emu) < 2e-5
