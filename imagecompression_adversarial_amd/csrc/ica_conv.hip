@@ -220,7 +220,10 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float nv = nacc[4 * g + e];
-            const float s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
+            // bf16 path: v_rsq_f32 / v_sqrt_f32 (1 ulp; n >= beta' > 0), no IEEE division / sqrt fix-ups
+            float s;
+            if constexpr (BF) s = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+            else s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
             sv[e] = s;
             yv[e] = acc[ct][4 * g + e] * s;
           }
@@ -276,7 +279,12 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           }
       }
     }
-    f32x16 tt[IT];
+    // t = (g x) dS/dn with x = y / s (in_x holds the GDN output y).  fp32 path: IEEE divisions, the op order
+    // the parity tests were pinned with.  bf16 path: GDN -0.5 g y s^2, IGDN 0.5 g y rcp(s)^2 (v_rcp_f32; the
+    // epilogue was VALU-bound on division sequences), and t goes straight into its hi/lo B fragments
+    // (register r = 4g+e is k-step r>>3, element r&7), no fp32 copy kept.
+    f32x16 tt[BF ? 1 : IT];
+    bf16x8 th[BF ? IT : 1][2], tl[BF ? IT : 1][2];
     const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
 #pragma unroll
     for (int it = 0; it < IT; ++it)
@@ -288,18 +296,34 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           xv = IX.ld(vo, ss);
           sv = IS.ld(vo, ss);
         }
+        f32x4 tv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float s = sv[e];
-          const float gx = acc[it][4 * g + e] * (xv[e] / s);  // in_x holds y = x*s: x = y / s
-          tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
+          float t;
+          if constexpr (!BF) {
+            const float gx = acc[it][4 * g + e] * (xv[e] / s);
+            t = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
+          } else if constexpr (EPI == EPI_GDN_BWD) {
+            t = (-0.5f * (acc[it][4 * g + e] * xv[e])) * (s * s);
+          } else {
+            const float r = __builtin_amdgcn_rcpf(s);
+            t = (0.5f * (acc[it][4 * g + e] * xv[e])) * (r * r);
+          }
+          tv[e] = t;
+          if constexpr (BF) {
+            __bf16 hi, lo;
+            split_bf(t, hi, lo);
+            th[it][g >> 1][4 * (g & 1) + e] = hi;
+            tl[it][g >> 1][4 * (g & 1) + e] = lo;
+          } else {
+            tt[it][4 * g + e] = t;
+          }
         }
         if constexpr ((FX & FX_T) != 0) {
-          if (valid) ST.st(vo, ss, f32x4{tt[it][4 * g], tt[it][4 * g + 1], tt[it][4 * g + 2], tt[it][4 * g + 3]});
+          if (valid) ST.st(vo, ss, tv);
         }
       }
-    // bf16: t is split into hi/lo B fragments on the fly per (jt, ct) (keeping all IT*4 split fragments
-    // live beside acc and t does not fit 256 registers)
     const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) {
@@ -311,17 +335,9 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
-            bf16x8 th, tl;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              __bf16 hi, lo;
-              split_bf(tt[ct][8 * s + j], hi, lo);
-              th[j] = hi;
-              tl[j] = lo;
-            }
-            uacc = mfma32bf(ah, th, uacc);
-            uacc = mfma32bf(al, th, uacc);
-            uacc = mfma32bf(ah, tl, uacc);
+            uacc = mfma32bf(ah, th[ct][s], uacc);
+            uacc = mfma32bf(al, th[ct][s], uacc);
+            uacc = mfma32bf(ah, tl[ct][s], uacc);
           }
         } else {
           const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
@@ -338,15 +354,19 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const unsigned ss = so(jt * 8 + 2 * g);
           const f32x4 xv = IX.ld(vo, ss), sv = IS.ld(vo, ss);
           f32x4 v;
+          // dx = g s + 2 x u,  x = y / s (bf16 path: y * rcp(s))
+          f32x4 xs;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xs[e] = BF ? xv[e] * __builtin_amdgcn_rcpf(sv[e]) : xv[e] / sv[e];
           if constexpr (STASH) {
             const f32x4 gs = Y.ld(vo, ss);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * (xv[e] / sv[e]) * uacc[4 * g + e];
+            for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * xs[e] * uacc[4 * g + e];
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const int r = 4 * g + e;
-              v[e] = acc[jt][r] * sv[e] + 2.0f * (xv[e] / sv[e]) * uacc[r];
+              v[e] = acc[jt][r] * sv[e] + 2.0f * xs[e] * uacc[r];
             }
           }
           Y.st(vo, ss, v);
