@@ -167,9 +167,11 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
-    // bf16 path: x^2 as the B operand of a bf16x3 GEMM (hi*hi + lo*hi + hi*lo), the accumulator
-    // registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives the matching gamma' order)
-    bf16x8 xh[BF ? IT : 1][2], xl[BF ? IT : 1][2];
+    // bf16 path: x^2 (rounded to bf16) as the B operand of a GEMM with gamma' as bf16 hi + lo (2 MFMAs per
+    // k-step); the accumulator registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives the
+    // matching gamma' order).  n then carries a <= 2^-9 relative error, s and y half of it, below the bf16
+    // rounding of the stored y and s.
+    bf16x8 xh[BF ? IT : 1][2];
     const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
     if constexpr (BF) {
 #pragma unroll
@@ -179,10 +181,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float xv = acc[it][8 * s + j];
-            __bf16 hi, lo;
-            split_bf(xv * xv, hi, lo);
-            xh[it][s][j] = hi;
-            xl[it][s][j] = lo;
+            xh[it][s][j] = (__bf16)(xv * xv);
           }
     }
 #pragma unroll
@@ -199,7 +198,6 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
             const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
             nacc = mfma32bf(ah, xh[it][s], nacc);
             nacc = mfma32bf(al, xh[it][s], nacc);
-            nacc = mfma32bf(ah, xl[it][s], nacc);
           }
         } else {
           const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
@@ -248,133 +246,208 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // Residual gradient: added unconditionally (r = 0 without one) so that the accumulators are
     // never live in two versions across a branch (that doubled the register footprint).
     const Img Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
-    if constexpr ((FX & FX_RES) != 0) {
-      const Img SX(p.save_x, img, n), RS(p.res, img, n);
+    if constexpr (BF) {
+      // bf16 path (FX == 0, IT <= 4): ONE pass over the saved (y, s) — the second read of them was the
+      // epilogue's latency cost at 2 waves/SIMD.  Per element: t (-> a bf16 B fragment), g*s in place of g,
+      // and 2x = 2 y rcp(s) kept as bf16 (the saved y and s are bf16 already); then per output tile
+      // u = gamma'^T t (gamma' as bf16 hi + lo: 2 MFMAs per k-step) and dx = g s + 2x u, stores only.
+      // t and 2x rounded to bf16 add 2^-9-relative errors, the size of the bf16 storage of y and s.
+      static_assert(!BF || (FX == 0 && IT <= 4), "bf16 GDN-bwd epilogue: plain, IT <= 4");
+      bf16x8 th[IT][2];
+      u32x2 x2q[IT][4];
+      // unconditional loads (one basic block, all in flight): a pixel outside the output reads past the
+      // descriptor's range (returns 0); its MFMA column (lanes j, j+32 = one pixel) is never stored
+      const unsigned vo_ld = valid ? vo : 0x1FFFFFF0u;
+      __builtin_amdgcn_sched_barrier(0);  // not into the main loop (its weight ring is live there)
 #pragma unroll
       for (int it = 0; it < IT; ++it)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const unsigned ss = so(it * 8 + 2 * g);
-          f32x4 r = {0.f, 0.f, 0.f, 0.f};
-          if (p.res && valid) r = RS.ld(vo, ss);
+          const f32x4 yv = IX.ld(vo_ld, ss), sv = IS.ld(vo_ld, ss);
+          f32x4 x2;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
-          if (p.save_x && valid)
-            SX.st(vo, ss, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
-        }
-    }
-    // IT > 4 (C = 192): g*s is parked in the output (same-thread global write, re-read below) so that
-    // the 6 accumulator tiles are dead while the 6 t tiles and the u GEMM are live.
-    constexpr bool STASH = IT > 4;
-    if constexpr (STASH) {
-      if (valid) {
-#pragma unroll
-        for (int it = 0; it < IT; ++it)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const unsigned ss = so(it * 8 + 2 * g);
-            const f32x4 sv = IS.ld(vo, ss);
-            Y.st(vo, ss, f32x4{acc[it][4 * g] * sv[0], acc[it][4 * g + 1] * sv[1], acc[it][4 * g + 2] * sv[2],
-                               acc[it][4 * g + 3] * sv[3]});
+          for (int e = 0; e < 4; ++e) {
+            const float gg = acc[it][4 * g + e], sg = sv[e], yg = yv[e];
+            const float r = __builtin_amdgcn_rcpf(sg);
+            const float t = (EPI == EPI_GDN_BWD) ? (-0.5f * (gg * yg)) * (sg * sg) : (0.5f * (gg * yg)) * (r * r);
+            th[it][g >> 1][4 * (g & 1) + e] = (__bf16)t;
+            float gs = gg * sg;
+            asm volatile("" : "+v"(gs));  // materialise here: LLVM otherwise sinks g*s and y*rcp(s) into the
+            acc[it][4 * g + e] = gs;      // stores after the GEMM, keeping g, s, y, r live (spills)
+            x2[e] = 2.0f * (yg * r);
           }
-      }
-    }
-    // t = (g x) dS/dn with x = y / s (in_x holds the GDN output y).  fp32 path: IEEE divisions, the op order
-    // the parity tests were pinned with.  bf16 path: GDN -0.5 g y s^2, IGDN 0.5 g y rcp(s)^2 (v_rcp_f32; the
-    // epilogue was VALU-bound on division sequences), and t goes straight into its hi/lo B fragments
-    // (register r = 4g+e is k-step r>>3, element r&7), no fp32 copy kept.
-    f32x16 tt[BF ? 1 : IT];
-    bf16x8 th[BF ? IT : 1][2], tl[BF ? IT : 1][2];
-    const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
-#pragma unroll
-    for (int it = 0; it < IT; ++it)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const unsigned ss = so(it * 8 + 2 * g);
-        f32x4 xv = {0.f, 0.f, 0.f, 0.f}, sv = {1.f, 1.f, 1.f, 1.f};
-        if (valid) {
-          xv = IX.ld(vo, ss);
-          sv = IS.ld(vo, ss);
+          u32x2 q = f4_to_bf4(x2);
+          asm volatile("" : "+v"(q));
+          x2q[it][g] = q;
         }
-        f32x4 tv;
+      __builtin_amdgcn_sched_barrier(0);  // pack 2x here, do not sink y and rcp(s) into the second phase
+      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float s = sv[e];
-          float t;
-          if constexpr (!BF) {
-            const float gx = acc[it][4 * g + e] * (xv[e] / s);
-            t = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
-          } else if constexpr (EPI == EPI_GDN_BWD) {
-            t = (-0.5f * (acc[it][4 * g + e] * xv[e])) * (s * s);
-          } else {
-            const float r = __builtin_amdgcn_rcpf(s);
-            t = (0.5f * (acc[it][4 * g + e] * xv[e])) * (r * r);
-          }
-          tv[e] = t;
-          if constexpr (BF) {
-            __bf16 hi, lo;
-            split_bf(t, hi, lo);
-            th[it][g >> 1][4 * (g & 1) + e] = hi;
-            tl[it][g >> 1][4 * (g & 1) + e] = lo;
-          } else {
-            tt[it][4 * g + e] = t;
-          }
-        }
-        if constexpr ((FX & FX_T) != 0) {
-          if (valid) ST.st(vo, ss, tv);
-        }
-      }
-    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
+      for (int jt = 0; jt < IT; ++jt) {
+        // keep each output tile's gamma'^T fragment loads inside its tile (hoisting all of them spilled)
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 uacc = f32x16{0};
 #pragma unroll
-    for (int jt = 0; jt < IT; ++jt) {
-      f32x16 uacc = f32x16{0};
-#pragma unroll
-      for (int ct = 0; ct < IT; ++ct) {
-        if constexpr (BF) {
+        for (int ct = 0; ct < IT; ++ct) {
           const int o = (jt * IT + ct) * 4096;
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
             uacc = mfma32bf(ah, th[ct][s], uacc);
             uacc = mfma32bf(al, th[ct][s], uacc);
-            uacc = mfma32bf(ah, tl[ct][s], uacc);
           }
-        } else {
-          const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
-          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+        }
+        if (valid) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 x2 = bf4_to_f4(x2q[jt][g]);
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + x2[e] * uacc[4 * g + e];
+            Y.st(vo, so(jt * 8 + 2 * g), v);
+          }
         }
       }
-      if (valid) {
-#pragma unroll
+    } else {
+      if constexpr ((FX & FX_RES) != 0) {
+        const Img SX(p.save_x, img, n), RS(p.res, img, n);
+  #pragma unroll
+        for (int it = 0; it < IT; ++it)
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const unsigned ss = so(it * 8 + 2 * g);
+            f32x4 r = {0.f, 0.f, 0.f, 0.f};
+            if (p.res && valid) r = RS.ld(vo, ss);
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
+            if (p.save_x && valid)
+              SX.st(vo, ss, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+          }
+      }
+      // IT > 4 (C = 192): g*s is parked in the output (same-thread global write, re-read below) so that
+      // the 6 accumulator tiles are dead while the 6 t tiles and the u GEMM are live.
+      constexpr bool STASH = IT > 4;
+      if constexpr (STASH) {
+        if (valid) {
+  #pragma unroll
+          for (int it = 0; it < IT; ++it)
+  #pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const unsigned ss = so(it * 8 + 2 * g);
+              const f32x4 sv = IS.ld(vo, ss);
+              Y.st(vo, ss, f32x4{acc[it][4 * g] * sv[0], acc[it][4 * g + 1] * sv[1], acc[it][4 * g + 2] * sv[2],
+                                 acc[it][4 * g + 3] * sv[3]});
+            }
+        }
+      }
+      // t = (g x) dS/dn with x = y / s (in_x holds the GDN output y).  fp32 path: IEEE divisions, the op order
+      // the parity tests were pinned with.  bf16 path: GDN -0.5 g y s^2, IGDN 0.5 g y rcp(s)^2 (v_rcp_f32; the
+      // epilogue was VALU-bound on division sequences), and t goes straight into its hi/lo B fragments
+      // (register r = 4g+e is k-step r>>3, element r&7), no fp32 copy kept.
+      f32x16 tt[BF ? 1 : IT];
+      bf16x8 th[BF ? IT : 1][2], tl[BF ? IT : 1][2];
+      const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
+  #pragma unroll
+      for (int it = 0; it < IT; ++it)
+  #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const unsigned ss = so(jt * 8 + 2 * g);
-          const f32x4 xv = IX.ld(vo, ss), sv = IS.ld(vo, ss);
-          f32x4 v;
-          // dx = g s + 2 x u,  x = y / s (bf16 path: y * rcp(s))
-          f32x4 xs;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) xs[e] = BF ? xv[e] * __builtin_amdgcn_rcpf(sv[e]) : xv[e] / sv[e];
-          if constexpr (STASH) {
-            const f32x4 gs = Y.ld(vo, ss);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * xs[e] * uacc[4 * g + e];
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int r = 4 * g + e;
-              v[e] = acc[jt][r] * sv[e] + 2.0f * xs[e] * uacc[r];
+          const unsigned ss = so(it * 8 + 2 * g);
+          f32x4 xv = {0.f, 0.f, 0.f, 0.f}, sv = {1.f, 1.f, 1.f, 1.f};
+          if (valid) {
+            xv = IX.ld(vo, ss);
+            sv = IS.ld(vo, ss);
+          }
+          f32x4 tv;
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float s = sv[e];
+            float t;
+            if constexpr (!BF) {
+              const float gx = acc[it][4 * g + e] * (xv[e] / s);
+              t = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
+            } else if constexpr (EPI == EPI_GDN_BWD) {
+              t = (-0.5f * (acc[it][4 * g + e] * xv[e])) * (s * s);
+            } else {
+              const float r = __builtin_amdgcn_rcpf(s);
+              t = (0.5f * (acc[it][4 * g + e] * xv[e])) * (r * r);
+            }
+            tv[e] = t;
+            if constexpr (BF) {
+              __bf16 hi, lo;
+              split_bf(t, hi, lo);
+              th[it][g >> 1][4 * (g & 1) + e] = hi;
+              tl[it][g >> 1][4 * (g & 1) + e] = lo;
+            } else {
+              tt[it][4 * g + e] = t;
             }
           }
-          Y.st(vo, ss, v);
+          if constexpr ((FX & FX_T) != 0) {
+            if (valid) ST.st(vo, ss, tv);
+          }
+        }
+      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
+  #pragma unroll
+      for (int jt = 0; jt < IT; ++jt) {
+        f32x16 uacc = f32x16{0};
+  #pragma unroll
+        for (int ct = 0; ct < IT; ++ct) {
+          if constexpr (BF) {
+            const int o = (jt * IT + ct) * 4096;
+  #pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
+              uacc = mfma32bf(ah, th[ct][s], uacc);
+              uacc = mfma32bf(al, th[ct][s], uacc);
+              uacc = mfma32bf(ah, tl[ct][s], uacc);
+            }
+          } else {
+            const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
+            const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+            const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                                  g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+          }
+        }
+        if (valid) {
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const unsigned ss = so(jt * 8 + 2 * g);
+            const f32x4 xv = IX.ld(vo, ss), sv = IS.ld(vo, ss);
+            f32x4 v;
+            // dx = g s + 2 x u,  x = y / s (bf16 path: y * rcp(s))
+            f32x4 xs;
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) xs[e] = BF ? xv[e] * __builtin_amdgcn_rcpf(sv[e]) : xv[e] / sv[e];
+            if constexpr (STASH) {
+              const f32x4 gs = Y.ld(vo, ss);
+  #pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * xs[e] * uacc[4 * g + e];
+            } else {
+  #pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int r = 4 * g + e;
+                v[e] = acc[jt][r] * sv[e] + 2.0f * xs[e] * uacc[r];
+              }
+            }
+            Y.st(vo, ss, v);
+          }
         }
       }
     }
   }
 }
+
+// bf16 weight-fragment load of tile it at step g (timing-only ICA_ABLATE_WLOAD build: no weight traffic,
+// synthetic small values, wrong results)
+#ifdef ICA_ABLATE_WLOAD
+#define ICA_WLOAD_BF(w, it, g) \
+  __builtin_bit_cast(bf16x8, (u32x4_t){0x3c003c00u + (unsigned)(((g) + (it)) & 7), 0x3c003c00u, 0x3c003c00u, \
+                                       0x3c003c00u + (unsigned)(threadIdx.x & 3)})
+#else
+#define ICA_WLOAD_BF(w, it, g) ((w)[(it) * 64])
+#endif
 
 // Load one (chunk, tap) weight fragment set: IT tiles x KH floats per lane.
 template <int IT, int KH>
@@ -508,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
     auto ldw = [&](bf16x8 (&a)[IT], int g) {
       const bf16x8* w = wb + (size_t)min(g, TG - 1) * IT * 64;
 #pragma unroll
-      for (int it = 0; it < IT; ++it) a[it] = w[it * 64];
+      for (int it = 0; it < IT; ++it) a[it] = ICA_WLOAD_BF(w, it, g);
     };
     auto tapoff = [&](int t) {
       t = min(t, KK - 1);  // taps past KK carry zero weights; read any finite patch value
@@ -545,7 +618,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
     auto ldw = [&](bf16x8 (&a)[IT], int g) {
       const bf16x8* w = wb + (size_t)min(g, total - 1) * IT * 64;
 #pragma unroll
-      for (int it = 0; it < IT; ++it) a[it] = w[it * 64];
+      for (int it = 0; it < IT; ++it) a[it] = ICA_WLOAD_BF(w, it, g);
     };
     auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int g) {
       const int ch = g / KK, tap = g - ch * KK;
@@ -660,7 +733,7 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
       auto ldw = [&](bf16x8 (&a)[IT], int u) {
         const bf16x8* w = wb + woff(min(u, total - 1)) * IT * 64;
 #pragma unroll
-        for (int it = 0; it < IT; ++it) a[it] = w[it * 64];
+        for (int it = 0; it < IT; ++it) a[it] = ICA_WLOAD_BF(w, it, u);
       };
       auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int u) {
         ldw(nxt, u + 3);
