@@ -46,7 +46,7 @@ def attack_(im_s, net, args):
         raise NotImplementedError("-p/--pad (reflect padding) is not supported on the HIP path")
     if getattr(args, "defend", False):
         raise NotImplementedError("--defend is not supported (it crashes inside the reference step loop)")
-    kern = net.kernels()
+    kern = net.kernels(getattr(args, "precision", "fp32"))
     init_noise = None
     if args.random > 1:
         init_noise = torch.empty_like(im_s).uniform_(-1e-2, 1e-2)

@@ -487,12 +487,18 @@ class CompressionModel(nn.Module):
                         getattr(mod, b).resize_(state_dict[key].size())
         return super().load_state_dict(state_dict, strict=strict)
 
-    def kernels(self):
-        """Whole-model HIP executor (used by the attack engine)."""
-        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+    def kernels(self, precision: str = "fp32"):
+        """Whole-model HIP executor (used by the attack engine).  precision 'bf16': bf16-operand g_a / g_s
+        convs (bmshj2018 models; BASELINE config 5)."""
+        key = (precision,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
         if getattr(self, "_ck", None) is None or self._ck_key != key:
             sd = {k: v.detach() for k, v in self.state_dict().items()}
-            self._ck = EC.ChengKernels(sd) if self.model_kind == "cheng2020" else E.CodecKernels(sd, self.model_kind)
+            if self.model_kind == "cheng2020":
+                if precision != "fp32":
+                    raise NotImplementedError("the bf16 conv path covers the bmshj2018 transforms")
+                self._ck = EC.ChengKernels(sd)
+            else:
+                self._ck = E.CodecKernels(sd, self.model_kind, precision=precision)
             self._ck_key = key
         return self._ck
 

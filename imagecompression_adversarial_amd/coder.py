@@ -179,4 +179,7 @@ def config():
                    help="seeded CompressAI-init weights instead of the zoo download (offline)")
     p.add_argument("--batch", dest="batch", type=int, default=1,
                    help="attack this many same-size images per launch (per-image semantics preserved)")
+    p.add_argument("--precision", dest="precision", type=str, default="fp32", choices=("fp32", "bf16"),
+                   help="g_a/g_s conv operands: fp32 (exact, the reference dtype) or bf16 (MFMA bf16, fp32 "
+                        "accumulate; BASELINE config 5)")
     return p

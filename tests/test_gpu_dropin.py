@@ -120,6 +120,19 @@ def test_attack_rd_cli_targeted_roi(capsys, tmp_path, monkeypatch):
     assert any(p.name.endswith("_advin_synthetic.png") for p in tmp_path.iterdir())
 
 
+def test_attack_rd_cli_bf16_targeted_roi(capsys, tmp_path, monkeypatch):
+    """Config 5 through the CLI: -t / --mask_loc on the bf16 conv path (--precision bf16)."""
+    from imagecompression_adversarial_amd import attack_rd, coder
+    monkeypatch.chdir(tmp_path)
+    args = coder.config().parse_args(["-m", "hyper", "-metric", "mse", "-q", "3", "-steps", "3", "-t", "synthetic",
+                                      "--mask_loc", "64", "192", "64", "192", "--precision", "bf16",
+                                      "-s", "synthetic:2x256x256", "--synthetic-weights", "--batch", "2"])
+    out = attack_rd.main(args)
+    txt = capsys.readouterr().out
+    assert "-> synthetic" in txt and "AVG: hyper-mse-3" in txt
+    assert out["bpp"] > 0
+
+
 def test_cheng2020_cli_runs(capsys):
     from imagecompression_adversarial_amd import attack_rd, coder
     args = coder.config().parse_args(["-m", "cheng2020", "-metric", "ms-ssim", "-q", "6", "-steps", "2",
