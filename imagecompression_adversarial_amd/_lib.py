@@ -57,6 +57,10 @@ _SIGS = {
     "ica_abs": [_p, _p, _l, _p],
     "ica_cast_f32_bf16": [_p, _p, _l, _p],
     "ica_cast_bf16_f32": [_p, _p, _l, _p],
+    # eval-time defences (ica_defend.hip)
+    "ica_flip_rot": [_p, _p, _l, _i, _i, _i, _p],
+    "ica_bitdepth": [_p, _p, _l, _f, _p],
+    "ica_resample_axis": [_p, _p, _l, _i, _i, _i, _i, _p, _p, _p, _i, _p],
     "ica_round": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],

@@ -1,0 +1,106 @@
+// Eval-time input defences of the reference's self_ensemble.py: the 8 dihedral
+// variants of the self-ensemble (rotates(), self_ensemble.py:34-57), bit-depth reduction
+// (bitdepth_reduction, :59-70) and the antialiased bicubic down/up resize (random_resize, :72-83, which is
+// torch.nn.functional.interpolate(mode="bicubic", antialias=True)).
+//
+// All three are HBM-bound gathers / stencils on NCHW fp32 planes (N = batch * channels planes).  The resize
+// is separable: one launch per axis applies host-built weight tables (xmin, xsize, K weights per output
+// index, torch's float32 _compute_weights_aa restated in self_ensemble.aa_table), so the kernel is a plain
+// K-tap gather; consecutive lanes take consecutive output columns (coalesced rows on both axes).
+#include "ica_common.h"
+
+// op 0: flip dim 2 (rows)   op 1: flip dim 3 (columns)
+// op 2: torch.rot90(x, 1, [2, 3])  out[i][j] = x[j][W-1-i]   (out is W x H)
+// op 3: torch.rot90(x, -1, [2, 3]) out[i][j] = x[H-1-j][i]   (out is W x H)
+__global__ void flip_rot_kernel(const float* __restrict__ x, float* __restrict__ y, long planes, int H, int W,
+                                int op) {
+  const int Ho = op >= 2 ? W : H, Wo = op >= 2 ? H : W;
+  const long plane = (long)H * W;
+  const long total = planes * plane;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long p = t / plane;
+    const long r = t - p * plane;
+    const int i = (int)(r / Wo), j = (int)(r - (long)i * Wo);
+    int si, sj;
+    if (op == 0) {
+      si = H - 1 - i;
+      sj = j;
+    } else if (op == 1) {
+      si = i;
+      sj = W - 1 - j;
+    } else if (op == 2) {
+      si = j;
+      sj = W - 1 - i;
+    } else {
+      si = H - 1 - j;
+      sj = i;
+    }
+    y[t] = x[p * plane + (long)si * W + sj];
+  }
+}
+
+// torch.round(x * scale) / scale  (round half to even; no contraction, the reference's float32 ops)
+__global__ void bitdepth_kernel(const float* __restrict__ x, float* __restrict__ y, long n, float scale) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = __fdiv_rn(rintf(__fmul_rn(x[i], scale)), scale);
+}
+
+// One separable pass of the antialiased resize: axis 1 resamples columns (W -> out_len), axis 0 rows
+// (H -> out_len).  out = sum_{k < xsize[o]} w[o][k] * in[xmin[o] + k], accumulated in k order.
+__global__ void resample_axis_kernel(const float* __restrict__ x, float* __restrict__ y, long planes, int H, int W,
+                                     int axis, int out_len, const int* __restrict__ xmin,
+                                     const int* __restrict__ xsize, const float* __restrict__ wt, int K) {
+  const int Ho = axis == 0 ? out_len : H, Wo = axis == 1 ? out_len : W;
+  const long oplane = (long)Ho * Wo, iplane = (long)H * W;
+  const long total = planes * oplane;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long p = t / oplane;
+    const long r = t - p * oplane;
+    const int i = (int)(r / Wo), j = (int)(r - (long)i * Wo);
+    const int o = axis == 1 ? j : i;
+    const int x0 = xmin[o], n = xsize[o];
+    const float* w = wt + (long)o * K;
+    const float* src = x + p * iplane;
+    float acc = 0.f;
+    if (axis == 1) {
+      const float* row = src + (long)i * W + x0;
+      for (int k = 0; k < n; ++k) acc += w[k] * row[k];
+    } else {
+      const float* col = src + (long)x0 * W + j;
+      for (int k = 0; k < n; ++k) acc += w[k] * col[(long)k * W];
+    }
+    y[t] = acc;
+  }
+}
+
+static inline int grid_1d_def(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+extern "C" {
+
+int ica_flip_rot(const float* x, float* y, long planes, int H, int W, int op, hipStream_t st) {
+  if (op < 0 || op > 3) return -5;
+  hipLaunchKernelGGL(flip_rot_kernel, dim3(grid_1d_def(planes * H * W)), dim3(256), 0, st, x, y, planes, H, W, op);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_bitdepth(const float* x, float* y, long n, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(bitdepth_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, x, y, n, scale);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_resample_axis(const float* x, float* y, long planes, int H, int W, int axis, int out_len, const int* xmin,
+                      const int* xsize, const float* w, int K, hipStream_t st) {
+  if (axis != 0 && axis != 1) return -5;
+  const long total = planes * (axis == 0 ? (long)out_len * W : (long)H * out_len);
+  hipLaunchKernelGGL(resample_axis_kernel, dim3(grid_1d_def(total)), dim3(256), 0, st, x, y, planes, H, W, axis,
+                     out_len, xmin, xsize, w, K);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

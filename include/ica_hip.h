@@ -74,6 +74,18 @@ int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bia
  * kernel reads bf16 x and writes fp32 y.  Casts for the tensors that leave the path (n % 4 == 0): */
 int ica_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
 int ica_cast_bf16_f32(const void* x, float* y, long n, hipStream_t stream);
+
+/* ---- eval-time defences (ica_defend.hip; self_ensemble.py:34-83) ------------------- */
+/* NCHW planes (planes = batch * channels).  op 0 flip rows, 1 flip columns, 2 torch.rot90(k=1, dims [2,3]),
+ * 3 rot90(k=-1); ops 2/3 write W x H planes. */
+int ica_flip_rot(const float* x, float* y, long planes, int H, int W, int op, hipStream_t stream);
+/* y = round_half_even(x * scale) / scale (self_ensemble.bitdepth_reduction, inference=True; scale = 2^bits - 1) */
+int ica_bitdepth(const float* x, float* y, long n, float scale, hipStream_t stream);
+/* one separable pass of the antialiased bicubic resize (F.interpolate(..., "bicubic", antialias=True)):
+ * axis 1 maps columns W -> out_len, axis 0 rows H -> out_len; out[o] = sum_{k<xsize[o]} w[o*K+k] in[xmin[o]+k];
+ * the tables are device arrays built on the host (self_ensemble.aa_table). */
+int ica_resample_axis(const float* x, float* y, long planes, int H, int W, int axis, int out_len, const int* xmin,
+                      const int* xsize, const float* w, int K, hipStream_t stream);
 /* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
  * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
  * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,

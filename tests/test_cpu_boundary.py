@@ -90,3 +90,28 @@ def test_lr_schedule_matches_torch():
     from oracle.attack import lr_schedule
     for steps in (1001, 100, 12, 3):
         assert _lr_table(steps, 0.01) == lr_schedule(steps, 0.01)
+
+
+def test_aa_table_matches_torch_antialias_weights():
+    """self_ensemble.aa_table (host logic) restates torch's float32 antialiased-bicubic weights: applying the
+    tables on the CPU reproduces F.interpolate(..., antialias=True) to 2e-6."""
+    import numpy as np
+    import torch.nn.functional as F
+    from imagecompression_adversarial_amd.self_ensemble import aa_table
+    g = torch.Generator().manual_seed(0)
+    for (H, W), sf in (((64, 96), 243 / 256), ((60, 91), 256 / 243), ((48, 40), 0.5)):
+        x = torch.rand((1, 3, H, W), generator=g)
+        ref = F.interpolate(x, scale_factor=sf, mode="bicubic", align_corners=False, antialias=True)
+        Ho, Wo = ref.shape[2:]
+        t = x.numpy()
+        for axis, n_in, n_out in ((3, W, Wo), (2, H, Ho)):
+            xmin, xsize, wt = aa_table(n_in, n_out, sf)
+            t = np.moveaxis(t, axis, -1)
+            o = np.zeros(t.shape[:-1] + (n_out,), np.float32)
+            for i in range(n_out):
+                acc = np.zeros(t.shape[:-1], np.float32)
+                for k in range(xsize[i]):
+                    acc = (acc + wt[i, k] * t[..., xmin[i] + k]).astype(np.float32)
+                o[..., i] = acc
+            t = np.moveaxis(o, -1, axis)
+        assert float(np.abs(t - ref.numpy()).max()) < 2e-6
