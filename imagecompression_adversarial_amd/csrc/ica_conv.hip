@@ -482,9 +482,15 @@ ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
 // [cb][chunk][tap][it][lane][KH]  with  o = cb*IT*32 + it*32 + (lane&31),
 // c = chunk*CC + (lane>>5)*KH + s.
 // --------------------------------------------------------------------------
+// pixel tiles (32 px each) per wave: the bf16 16-channel-chunk path runs 2, so each weight fragment (an
+// L1 -> register stream of 4 KB per wave-step, the bf16 main loop's limit) feeds twice the MFMAs
+template <int CC, bool BF>
+constexpr int down_pt() { return (BF && CC == 16) ? 2 : 1; }
+
 template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
 __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
-  constexpr int TH = 128 / TW;
+  constexpr int PT = down_pt<CC, BF>();
+  constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
   constexpr int NQ = CC / 4, KH = CC / 2, PLANE = PR * PC, PAD = KS / 2;
   constexpr int WSTEP = IT * 64 * KH;  // floats per (chunk, tap)
@@ -503,15 +509,24 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
   const int n = bid / tiles_y;
   const int cb = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-  const int pl = wave * 32 + j, oyl = pl / TW, oxl = pl % TW;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
   const int Cin4 = (p.Cin + 3) >> 2;
   const int nch = (Cin4 * 4 + CC - 1) / CC;
-
-  f32x16 acc[IT];
+  // pixel tile t of this wave: block pixels (wave*PT + t)*32 + j
+  int oyl[PT], oxl[PT];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+  for (int t = 0; t < PT; ++t) {
+    const int pl = (wave * PT + t) * 32 + j;
+    oyl[t] = pl / TW;
+    oxl[t] = pl % TW;
+  }
+
+  f32x16 acc[PT][IT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
 
   // one 4-channel group of the conv input at (iy, ix), with the fill-mode view applied
   auto ldc4 = [&](int c4, int iy, int ix) -> f32x4 {
@@ -569,7 +584,10 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 
   constexpr int KK = KS * KS;
   const int total = nch * KK;
-  const int lbase = (S * oyl) * PC + S * oxl;
+  int lb[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) lb[t] = (S * oyl[t]) * PC + S * oxl[t];
+  const int lbase = lb[0];
   if constexpr (BF && CC == 4) {
     // bf16, 3-channel input: k = 8h + j of tap group tg is tap 4tg + 2h + (j>>2), channel j&3, so a lane's
     // B fragment is the f32x4 pixels of two taps (rounded to bf16); 7 MFMAs per tile cover the 25 taps
@@ -593,7 +611,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
       const int t0 = 4 * g + 2 * h;
       const bf16x8 b = to_bf8(patch[tapoff(t0)], patch[tapoff(t0 + 1)]);
 #pragma unroll
-      for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], b, acc[it]);
+      for (int it = 0; it < IT; ++it) acc[0][it] = mfma32bf(cur[it], b, acc[0][it]);
     };
     ldw(fr[0], 0);
     ldw(fr[1], 1);
@@ -625,9 +643,13 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
       if (tap == 0) fill(ch);
       ldw(nxt, g + 3);
       const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-      const bf16x8 b = f4_as_bf8(patch[h * PLANE + lbase + ky * PC + kx]);
+      bf16x8 b[PT];
 #pragma unroll
-      for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], b, acc[it]);
+      for (int t = 0; t < PT; ++t) b[t] = f4_as_bf8(patch[h * PLANE + lb[t] + ky * PC + kx]);
+#pragma unroll
+      for (int t = 0; t < PT; ++t)
+#pragma unroll
+        for (int it = 0; it < IT; ++it) acc[t][it] = mfma32bf(cur[it], b[t], acc[t][it]);
     };
     ldw(fr[0], 0);
     ldw(fr[1], 1);
@@ -672,7 +694,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 #pragma unroll
       for (int s2 = 0; s2 < KH; ++s2)
 #pragma unroll
-        for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+        for (int it = 0; it < IT; ++it) acc[0][it] = mfma32(cur[it][s2], b[s2], acc[0][it]);
     };
     float fa[IT][KH], fb[IT][KH];
     load_frag<IT, KH>(fa, wptr);
@@ -684,8 +706,11 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
     }
     if (g < total) step(fa, fb, g);
   }
-  const int oy = oy0 + oyl, ox = ox0 + oxl;
-  conv_epilogue<IT, EPI, FX, BF>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int oy = oy0 + oyl[t], ox = ox0 + oxl[t];
+    conv_epilogue<IT, EPI, FX, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -1100,7 +1125,7 @@ constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) ||
 
 template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
 static int launch_down(const ConvParams& p, hipStream_t st) {
-  constexpr int TH = 128 / TW;
+  constexpr int TH = down_pt<CC, BF>() * 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
   hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF>), grid, dim3(256), 0, st, p);
