@@ -309,6 +309,54 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           }
         }
       }
+    } else if constexpr (FX == 0 && IT <= 4) {
+      // fp32, plain layers: one pass over the saved (y, s) as well.  x = y / s, t and g*s are formed with the
+      // ops of the two-pass form below and kept in registers (gs in place of g), so dx needs no second read.
+      f32x16 tt[IT], xx[IT];
+      const unsigned vo_ld = valid ? vo : 0x0FFFFFF0u;  // past the descriptor's range: loads return 0
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const unsigned ss = so(it * 8 + 2 * g);
+          const f32x4 yv = IX.ld(vo_ld, ss), sv = IS.ld(vo_ld, ss);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sg = sv[e], xs = yv[e] / sg;
+            const float gx = acc[it][4 * g + e] * xs;
+            tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
+            float gs = acc[it][4 * g + e] * sg;
+            float x2 = 2.0f * xs;
+            asm volatile("" : "+v"(gs), "+v"(x2));  // materialise (see the bf16 branch)
+            acc[it][4 * g + e] = gs;
+            xx[it][4 * g + e] = x2;
+          }
+        }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jt = 0; jt < IT; ++jt) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 uacc = f32x16{0};
+#pragma unroll
+        for (int ct = 0; ct < IT; ++ct) {
+          const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
+          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+#pragma unroll
+          for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+        }
+        if (valid) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + xx[jt][4 * g + e] * uacc[4 * g + e];
+            Y.st(vo, so(jt * 8 + 2 * g), v);
+          }
+        }
+      }
     } else {
       if constexpr ((FX & FX_RES) != 0) {
         const Img SX(p.save_x, img, n), RS(p.res, img, n);
