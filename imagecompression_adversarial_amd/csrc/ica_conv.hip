@@ -167,10 +167,10 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
-    // bf16 path: x^2 (rounded to bf16) as the B operand of a GEMM with gamma' as bf16 hi + lo (2 MFMAs per
-    // k-step); the accumulator registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives the
-    // matching gamma' order).  n then carries a <= 2^-9 relative error, s and y half of it, below the bf16
-    // rounding of the stored y and s.
+    // bf16 path: x^2 (rounded to bf16) as the B operand of a bf16 GEMM with gamma' (its bf16 hi part; one
+    // MFMA per k-step); the accumulator registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives
+    // the matching gamma' order).  n = beta' + sum of non-negative terms then carries <= 2^-8 relative error,
+    // s and y half of it: the size of the bf16 rounding of the stored y and s.
     bf16x8 xh[BF ? IT : 1][2];
     const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
     if constexpr (BF) {
@@ -194,11 +194,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         if constexpr (BF) {
           const int o = (ct * IT + it) * 4096;
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
-            nacc = mfma32bf(ah, xh[it][s], nacc);
-            nacc = mfma32bf(al, xh[it][s], nacc);
-          }
+          for (int s = 0; s < 2; ++s) nacc = mfma32bf(ld_bf8(grs, lane * 16, o + s * 2048), xh[it][s], nacc);
         } else {
           const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
           const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
@@ -250,8 +246,8 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       // bf16 path (FX == 0, IT <= 4): ONE pass over the saved (y, s) — the second read of them was the
       // epilogue's latency cost at 2 waves/SIMD.  Per element: t (-> a bf16 B fragment), g*s in place of g,
       // and 2x = 2 y rcp(s) kept as bf16 (the saved y and s are bf16 already); then per output tile
-      // u = gamma'^T t (gamma' as bf16 hi + lo: 2 MFMAs per k-step) and dx = g s + 2x u, stores only.
-      // t and 2x rounded to bf16 add 2^-9-relative errors, the size of the bf16 storage of y and s.
+      // u = gamma'^T t (bf16 MFMAs, gamma' hi part) and dx = g s + 2x u, stores only.  t, gamma' and 2x rounded
+      // to bf16 add 2^-9-relative errors, the size of the bf16 storage of y and s.
       static_assert(!BF || (FX == 0 && IT <= 4), "bf16 GDN-bwd epilogue: plain, IT <= 4");
       bf16x8 th[IT][2];
       u32x2 x2q[IT][4];
@@ -292,11 +288,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         for (int ct = 0; ct < IT; ++ct) {
           const int o = (jt * IT + ct) * 4096;
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
-            uacc = mfma32bf(ah, th[ct][s], uacc);
-            uacc = mfma32bf(al, th[ct][s], uacc);
-          }
+          for (int s = 0; s < 2; ++s) uacc = mfma32bf(ld_bf8(grs, lane * 16, o + s * 2048), th[ct][s], uacc);
         }
         if (valid) {
 #pragma unroll
@@ -766,7 +758,16 @@ __global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
 // y = 2a + PY uses taps ky = PY (mod 2) at input row iy = a + (PY + 2 - ky)/2.
 // Weight fragments packed [cb][tap][chunk][it][lane][8] (CC = 16).
 // --------------------------------------------------------------------------
-constexpr int UP_TH = 4, UP_TW = 16, UP_PR = UP_TH + 2, UP_PC = UP_TW + 2, UP_PLANE = UP_PR * UP_PC;
+// Block tile: UP_TH input rows x UP_TW input columns (4 parity classes of 2x as many output pixels).  The
+// bf16 path doubles the rows: each wave then runs two 32-pixel tiles per class (up_pt), so a weight
+// fragment feeds twice the MFMAs (as in conv_down).
+constexpr int UP_TW = 16, UP_PC = UP_TW + 2;
+template <bool BF>
+constexpr int up_pt() { return BF ? 2 : 1; }
+template <bool BF>
+constexpr int up_th() { return 4 * up_pt<BF>(); }
+template <bool BF>
+constexpr int up_plane() { return (up_th<BF>() + 2) * UP_PC; }
 
 // Generalised over the kernel size: ConvTranspose2d kKS s2 p(KS/2) op1, i.e. the input-gradient
 // of a stride-2 KSxKS conv with pad KS/2 (KS = 5: g_s deconvs / g_a dgrad; KS = 3, 1: the dgrad of
@@ -776,14 +777,18 @@ template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF>
 ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
                            int nch) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-  const int a_rel = jt * 2 + (j >> 4), b_rel = j & 15;
+  constexpr int PT = up_pt<BF>(), UP_PLANE = up_plane<BF>();
+  // pixel tile t of this wave: input rows (jt*PT + t)*2 + (j>>4) of the block tile, columns j&15
+  const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
   constexpr int WSTEP = IT * 64 * 8;
   constexpr int PAD = KS / 2;
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2;  // taps per axis
-  f32x16 acc[IT];
+  f32x16 acc[PT][IT];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+  for (int t = 0; t < PT; ++t)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
   // (tap, chunk) sequence flattened
   const int total = NY * NX * nch;
   auto woff = [&](int u) -> size_t {
@@ -810,9 +815,14 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
       };
       auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int u) {
         ldw(nxt, u + 3);
-        const bf16x8 b = f4_as_bf8(patch[poff(u)]);
+        const int po = poff(u);
+        bf16x8 b[PT];
 #pragma unroll
-        for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], b, acc[it]);
+        for (int t = 0; t < PT; ++t) b[t] = f4_as_bf8(patch[po + t * 2 * UP_PC]);   // tile t: 2 rows down
+#pragma unroll
+        for (int t = 0; t < PT; ++t)
+#pragma unroll
+          for (int it = 0; it < IT; ++it) acc[t][it] = mfma32bf(cur[it], b[t], acc[t][it]);
       };
       ldw(fr[0], 0);
       ldw(fr[1], 1);
@@ -839,7 +849,7 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2)
 #pragma unroll
-          for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+          for (int it = 0; it < IT; ++it) acc[0][it] = mfma32(cur[it][s2], b[s2], acc[0][it]);
       };
       float fa[IT][8], fb[IT][8];
       load_frag<IT, 8>(fa, wl + woff(0) * WSTEP);
@@ -852,13 +862,17 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
       if (u < total) step(fa, fb, u);
     }
   }
-  const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
-  conv_epilogue<IT, EPI, FX, BF>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
+    conv_epilogue<IT, EPI, FX, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  }
 }
 
 template <int KS, int IT, int EPI, int FX, bool BF>
 __global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
-  extern __shared__ f32x4 patch[];  // fp32: [Cin/4][UP_PR][UP_PC] f32x4; bf16: [Cin/8][UP_PR][UP_PC] bf16x8
+  extern __shared__ f32x4 patch[];  // fp32: [Cin/4][TH+2][UP_PC] f32x4; bf16: [Cin/8][TH+2][UP_PC] bf16x8
+  constexpr int UP_TH = up_th<BF>(), UP_PLANE = up_plane<BF>();
   const int Hh = p.Hin, Wh = p.Win;
   const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UP_TH - 1) / UP_TH;
   int bid = blockIdx.x;
@@ -1276,9 +1290,10 @@ static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, int fx
 template <int KS, int IT, int EPI, int FX, bool BF = false>
 static int launch_up(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
+  constexpr int UP_TH = up_th<BF>();
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  const size_t lds = (size_t)(p.Cin / (BF ? 8 : 4)) * UP_PLANE * sizeof(f32x4);
+  const size_t lds = (size_t)(p.Cin / (BF ? 8 : 4)) * up_plane<BF>() * sizeof(f32x4);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1493,7 +1508,8 @@ int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bia
   return 0;
 }
 
-// bf16x3 GDN fragments (prec = 1): for channel tiles (a, b), k-step s, part hl (0 = hi, 1 = lo), lane l:
+// bf16 GDN fragments (prec = 1; the epilogues read the hi part, lo is kept for a bf16x3 variant):
+// for channel tiles (a, b), k-step s, part hl (0 = hi, 1 = lo), lane l:
 // element j = part of M[a*32 + (l&31)][b*32 + 16s + 8(j>>2) + 4(l>>5) + (j&3)], the k order in which the
 // accumulator registers 8s..8s+7 of a 32x32 tile serve as the B operand.  M = gamma' or gamma'^T;
 // hi = bf16(g), lo = bf16(g - hi).  gpb holds (C/32)^2 * 2048 bf16; beta_eff as ica_pack_gdn.

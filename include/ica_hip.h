@@ -57,7 +57,8 @@ int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_e
  * ica_pack_conv_weight_bf16: the fragment order of ica_pack_conv_weight with CC = 16, each element rounded to
  *   bf16 (RNE); dst holds ica_pack_conv_weight_size(O, C, KS, 16, it) bf16 values.
  * ica_pack_gdn_bf16: gamma' (or gamma'^T) as bf16 hi/lo pairs in the k order of accumulator-as-operand MFMAs
- *   (the GDN normaliser / GDN-bwd GEMMs run bf16x3: hi*hi + lo*hi + hi*lo); gpb holds (C/32)^2 * 2048 bf16. */
+ *   (the GDN normaliser / GDN-bwd GEMMs use the hi part: bf16 is what the stored y and s carry; the lo part is
+ *   packed for a bf16x3 variant); gpb holds (C/32)^2 * 2048 bf16. */
 int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order,
                               int flip, int it, hipStream_t stream);
 int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* beta_eff, int C, int transpose,
