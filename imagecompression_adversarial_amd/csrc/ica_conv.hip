@@ -527,8 +527,13 @@ ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
 template <int CC, bool BF>
 constexpr int down_pt() { return (BF && CC == 16) ? 2 : 1; }
 
+// occupancy target: 2 blocks/CU, except the k5 IT = 6 (C = 192, bmshj2018 q6-8) variants, whose 6-tile
+// accumulators + fragment ring + GDN epilogue need the whole 512-register file (1 block/CU, no spills)
+template <int KS, int IT>
+constexpr int conv_min_blocks() { return (KS == 5 && IT == 6) ? 1 : 2; }
+
 template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
-__global__ __launch_bounds__(256, 2) void conv_down_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_kernel(ConvParams p) {
   constexpr int PT = down_pt<CC, BF>();
   constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
@@ -870,7 +875,7 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
 }
 
 template <int KS, int IT, int EPI, int FX, bool BF>
-__global__ __launch_bounds__(256, 2) void conv_up_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kernel(ConvParams p) {
   extern __shared__ f32x4 patch[];  // fp32: [Cin/4][TH+2][UP_PC] f32x4; bf16: [Cin/8][TH+2][UP_PC] bf16x8
   constexpr int UP_TH = up_th<BF>(), UP_PLANE = up_plane<BF>();
   const int Hh = p.Hin, Wh = p.Win;
@@ -1159,7 +1164,11 @@ constexpr bool down_base() {
   constexpr bool it_ok = IT == 1 || IT == 3 || IT == 4 || IT == 6;
   constexpr bool gdn = EPI >= EPI_GDN && EPI <= EPI_IGDN_BWD;
   if (!it_ok) return false;
-  if (KS == 5 && S == 2) return IT != 6 && (gdn ? IT == 4 : (EPI == EPI_BIAS || EPI == EPI_RELU));
+  if (KS == 5 && S == 2) {
+    // IT = 6: the C = 192 GDN layers of bmshj2018 q6-8 (g_a forward, g_s input-gradient)
+    if (IT == 6) return EPI == EPI_GDN || EPI == EPI_IGDN_BWD;
+    return gdn ? IT == 4 : (EPI == EPI_BIAS || EPI == EPI_RELU);
+  }
   if (KS == 3 && S == 1) return gdn ? (IT == 4 || IT == 6) : true;
   if (KS == 3 && S == 2) return EPI == EPI_BIAS || EPI == EPI_LRELU;
   if (KS == 1 && S == 2) return EPI == EPI_BIAS;
@@ -1326,6 +1335,15 @@ static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStre
       if (epi == EPI_BIAS) return launch_up<5, 1, EPI_BIAS, 0>(p, st);
       if (epi == EPI_RELU) return launch_up<5, 1, EPI_RELU, 0>(p, st);
       return -4;
+    }
+    if (it == 6) {  // C = 192 (bmshj2018 q6-8: g_s IGDN layers, g_a GDN input-gradients, h_s ReLU deconvs)
+      switch (epi) {
+        case EPI_BIAS: return launch_up<5, 6, EPI_BIAS, 0>(p, st);
+        case EPI_RELU: return launch_up<5, 6, EPI_RELU, 0>(p, st);
+        case EPI_IGDN: return launch_up<5, 6, EPI_IGDN, 0>(p, st);
+        case EPI_GDN_BWD: return launch_up<5, 6, EPI_GDN_BWD, 0>(p, st);
+        default: return -5;
+      }
     }
     if (it == 4) {
       switch (epi) {

@@ -32,7 +32,10 @@ class Analysis:
         self.tag = tag
         self.N = _P(sd, prefix, "0.weight").shape[0]
         self.M = _P(sd, prefix, "6.weight").shape[0]
-        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "conv", 2, prec)
+        # C = 192 GDN layers (q6-8) run 6 row tiles per wave: convs 0-2 forward, convs 1-3 input-gradient
+        g6 = 6 if self.N == 192 else 0
+        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "conv", 2, prec,
+                                   it_fwd=g6 if i < 6 else 0, it_bwd=g6 if i > 0 else 0)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
 
@@ -41,7 +44,7 @@ class Analysis:
         for i in range(3):
             p = self.convs[i]
             h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.gdns[i], save,
-                                    tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec)
+                                    tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd)
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
@@ -53,7 +56,8 @@ class Analysis:
         g, C = gy4, self.M
         for i in (3, 2, 1):
             g, _, _ = K.conv_up(g, C, self.convs[i].bwd, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
-                                saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec)
+                                saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
+                                it=self.convs[i].it_bwd)
             C = self.N
         gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad",
                              prec=self.convs[0].bwd_prec)
@@ -67,7 +71,10 @@ class Synthesis:
         self.tag = tag
         self.M = _P(sd, prefix, "0.weight").shape[0]
         self.N = _P(sd, prefix, "0.weight").shape[1]
-        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "deconv", 2, prec)
+        # C = 192 IGDN layers (q6-8): deconvs 0-2 forward, deconvs 1-3 input-gradient (conv_down into N channels)
+        g6 = 6 if self.N == 192 else 0
+        self.convs = [K.PackedConv(_P(sd, prefix, f"{i}.weight"), _P(sd, prefix, f"{i}.bias"), "deconv", 2, prec,
+                                   it_fwd=g6 if i < 6 else 0, it_bwd=g6 if i > 0 else 0)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
 
@@ -76,7 +83,7 @@ class Synthesis:
         for i in range(3):
             p = self.convs[i]
             h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gdns[i], save,
-                                  tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec)
+                                  tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd)
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
@@ -87,7 +94,8 @@ class Synthesis:
         g, C = gx4, 3
         for i in (3, 2, 1):
             g, _, _ = K.conv_down(g, C, self.convs[i].bwd, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gdns[i - 1],
-                                  saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec)
+                                  saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
+                                  it=self.convs[i].it_bwd)
             C = self.N
         gy, _, _ = K.conv_down(g, self.N, self.convs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS,
                                tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec)
@@ -119,14 +127,15 @@ class HyperSynthesis:
     def __init__(self, sd: dict, prefix: str = "h_s"):
         self.N = _P(sd, prefix, "0.weight").shape[0]
         self.M = _P(sd, prefix, "4.weight").shape[0]
-        self.convs = [K.PackedConv(_P(sd, prefix, "0.weight"), _P(sd, prefix, "0.bias"), "deconv", 2),
-                      K.PackedConv(_P(sd, prefix, "2.weight"), _P(sd, prefix, "2.bias"), "deconv", 2),
+        r6 = 6 if self.N == 192 else 0   # q6-8: ReLU deconvs into 192 channels (6 row tiles)
+        self.convs = [K.PackedConv(_P(sd, prefix, "0.weight"), _P(sd, prefix, "0.bias"), "deconv", 2, it_fwd=r6),
+                      K.PackedConv(_P(sd, prefix, "2.weight"), _P(sd, prefix, "2.bias"), "deconv", 2, it_fwd=r6),
                       K.PackedConv(_P(sd, prefix, "4.weight"), _P(sd, prefix, "4.bias"), "conv", 1)]
 
     def forward(self, z4):
         p0, p1, p2 = self.convs
-        s, _, _ = K.conv_up(z4, self.N, p0.fwd, p0.bias, self.N, K.EPI_RELU)
-        s, _, _ = K.conv_up(s, self.N, p1.fwd, p1.bias, self.N, K.EPI_RELU)
+        s, _, _ = K.conv_up(z4, self.N, p0.fwd, p0.bias, self.N, K.EPI_RELU, it=p0.it_fwd)
+        s, _, _ = K.conv_up(s, self.N, p1.fwd, p1.bias, self.N, K.EPI_RELU, it=p1.it_fwd)
         s, _, _ = K.conv_down(s, self.N, p2.fwd, p2.bias, self.M, 3, 1, K.EPI_RELU)
         return s
 

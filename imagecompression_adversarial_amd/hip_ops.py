@@ -151,9 +151,15 @@ class PackedConv:
     kind 'deconv' : nn.ConvTranspose2d weight [Cin][Cout][k][k]  fwd = conv_up, dgrad = conv_down
     """
 
-    def __init__(self, weight: torch.Tensor, bias, kind: str, stride: int, prec: int = PREC_FP32):
+    def __init__(self, weight: torch.Tensor, bias, kind: str, stride: int, prec: int = PREC_FP32,
+                 it_fwd: int = 0, it_bwd: int = 0):
         """prec=PREC_BF16 packs the k5 s2 layers as bf16 fragments (fwd_prec / bwd_prec record what each pack
-        is): 16-channel chunks, 4-tap groups for an RGB conv input, the Z-gather pack for 3-channel outputs."""
+        is): 16-channel chunks, 4-tap groups for an RGB conv input, the Z-gather pack for 3-channel outputs.
+        it_fwd / it_bwd: 32-channel row tiles per wave of the forward / input-gradient launches (0 = the library
+        default; 6 for the C = 192 GDN layers of bmshj2018 q6-8, whose epilogue needs all channels in one wave)."""
+        self.it_fwd, self.it_bwd = it_fwd, it_bwd
+        if prec == PREC_BF16 and (it_fwd or it_bwd):
+            raise NotImplementedError("the bf16 conv path covers the N = 128 transforms (q1-5)")
         self.kind = kind
         self.fwd_prec = self.bwd_prec = PREC_FP32
         self.stride = stride
@@ -167,7 +173,7 @@ class PackedConv:
                 self.fwd_prec = PREC_BF16
             else:
                 self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
-                                     conv_cc(self.Cin))
+                                     conv_cc(self.Cin), it=it_fwd)
             # dgrad: k5 s2 -> conv_up (o = ci, c = co); k3 s1 -> conv_down with the taps reversed
             self.bwd = None
             if self.KS == 3 and stride == 1 and self.Cout % 16 == 0:
@@ -181,7 +187,8 @@ class PackedConv:
                     self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP)
                     self.bwd_prec = PREC_BF16
                 else:
-                    self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16)
+                    self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16,
+                                         it=it_bwd)
         elif kind == "deconv":
             self.Cin, self.Cout = weight.shape[0], weight.shape[1]
             # forward (conv_up): o = co, c = ci
@@ -192,14 +199,15 @@ class PackedConv:
                 self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP)
                 self.fwd_prec = PREC_BF16
             else:
-                self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16)
+                self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16,
+                                     it=it_fwd)
             # dgrad (conv_down, stride 2): o = ci, c = co
             if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cout >= 16 or self.Cout <= 4):
                 self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN)
                 self.bwd_prec = PREC_BF16
             else:
                 self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,
-                                     conv_cc(self.Cout))
+                                     conv_cc(self.Cout), it=it_bwd)
         else:
             raise ValueError(kind)
         self.bias = None if bias is None else bias.detach().contiguous()
@@ -239,13 +247,14 @@ class PackedGDN:
 # Convolutions
 # --------------------------------------------------------------------------- #
 def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False,
-              saved=None, out=None, tag=None, save_t=None, prec=PREC_FP32):
+              saved=None, out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
     """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s).
     save_t: optional nChw4c output of t = dL/dn for the GDN-bwd epilogues (GDN parameter gradients).
-    prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex)."""
+    prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex).
+    it: the row-tile count wp was packed with (0 = library default; explicit values go through ica_conv_ex)."""
     N, _, H, W, _ = x4.shape
-    if prec == PREC_BF16:
-        return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t)
+    if prec == PREC_BF16 or it:
+        return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
     Wo = (W + 2 * (KS // 2) - KS) // S + 1
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
@@ -266,11 +275,11 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
 
 
 def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
-            out=None, tag=None, save_t=None, prec=PREC_FP32):
+            out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
-    if prec == PREC_BF16 and Cout != 3:
-        return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t)
+    if (prec == PREC_BF16 or it) and Cout != 3:
+        return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho, Wo = 2 * H, 2 * W
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
     if Cout == 3:
@@ -297,13 +306,15 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     return y, (y if ss is not None else None), ss
 
 
-def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out, tag, save_t):
-    """conv_down / conv_up semantics (returns (y4, save_x, save_s)) for a bf16-operand launch."""
+def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out, tag, save_t, prec, it):
+    """conv_down / conv_up semantics (returns (y4, save_x, save_s)) through ica_conv_ex: bf16-operand launches and
+    explicit row-tile counts."""
     N, _, H, W, _ = x4.shape
     Ho, Wo = ((H + 2 * (KS // 2) - KS) // S + 1, (W + 2 * (KS // 2) - KS) // S + 1) if kind == 0 else (2 * H, 2 * W)
-    ss = empty_nc4(N, Cout, Ho, Wo, x4.device, torch.bfloat16) if (save and epi in (EPI_GDN, EPI_IGDN)) else None
-    y = conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind, epi, 0, gdn, save_s=ss, saved=saved, save_t=save_t, out=out,
-                tag=tag, prec=PREC_BF16)
+    dt = torch.bfloat16 if prec == PREC_BF16 else torch.float32
+    ss = empty_nc4(N, Cout, Ho, Wo, x4.device, dt) if (save and epi in (EPI_GDN, EPI_IGDN)) else None
+    y = conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind, epi, it, gdn, save_s=ss, saved=saved, save_t=save_t, out=out,
+                tag=tag, prec=prec)
     return y, (y if ss is not None else None), ss
 
 

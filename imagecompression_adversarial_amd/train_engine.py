@@ -43,6 +43,9 @@ class RDTrainer:
             raise ValueError(f"metric {metric!r}: the HIP trainer supports mse and ms-ssim (lpips is out of scope)")
         self.net, self.metric, self.lmbda = net, metric, float(lmbda)
         self.kind = net.model_kind
+        if net.g_a[0].weight.shape[0] != 128:
+            raise NotImplementedError("the HIP train step covers N = 128 (quality 1-5); q6-8 (N = 192) runs the "
+                                      "attack / eval paths only")
         named = dict(net.named_parameters())
         self.names = sorted(n for n in named if not n.endswith(".quantiles"))
         self.params = {n: named[n] for n in self.names}

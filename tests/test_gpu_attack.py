@@ -226,3 +226,31 @@ def test_entropy_models_vs_oracle(hyper3):
     yr, ylr = codec.gaussian_conditional(y, sc)
     assert torch.equal(K.from_nc4(yh4, 192).cpu(), yr)
     assert rel_err(K.from_nc4(ylik4, 192).cpu(), ylr) < 1e-4
+
+
+@pytest.mark.parametrize("model", ["hyper", "factorized"])
+def test_quality6_n192_vs_oracle(model):
+    """bmshj2018 q6-8 (N = 192, M = 320): the C = 192 GDN layers run 6 row tiles per wave (k5 IT = 6 kernels).
+    g_a + g_s forward / input gradient and the eval forward (bpp) vs the oracle."""
+    from imagecompression_adversarial_amd import hip_ops as K
+    from imagecompression_adversarial_amd.engine import CodecKernels
+    P = codec.perturb_params(codec.init_params(model, 6, seed=0), seed=1)
+    assert P["g_a.0.weight"].shape[0] == 192 and P["g_a.6.weight"].shape[0] == 320
+    kern = CodecKernels({k: v.to(DEV) for k, v in P.items()}, model)
+    x = rnd((2, 3, 64, 128), 71)    # multiples of 64 (coder.read_image pads so)
+    xr = x.clone().requires_grad_(True)
+    y_ref = codec.g_a(P, xr)
+    xh_ref = codec.g_s(P, y_ref)
+    gout = rnd(xh_ref.shape, 72, -1, 1)
+    (xh_ref * gout).sum().backward()
+    y4, sa = kern.g_a(K.to_nc4(x.to(DEV)), save=True)
+    xh4, ss = kern.g_s(y4, save=True)
+    assert rel_err(K.from_nc4(y4, 320).cpu(), y_ref.detach()) < 1e-4
+    assert rel_err(K.from_nc4(xh4, 3).cpu(), xh_ref.detach()) < 1e-4
+    gx4 = kern.g_a_backward(kern.g_s_backward(K.to_nc4(gout.to(DEV)), ss), sa)
+    assert rel_err(K.from_nc4(gx4, 3).cpu(), xr.grad) < 1e-3
+    from imagecompression_adversarial_amd.attack import eval_forward
+    out, bpp = eval_forward(kern, x.to(DEV))
+    ref = codec.forward(P, x, model)
+    bref = torch.stack([codec.bpp({k: v[b:b + 1] for k, v in ref["likelihoods"].items()}, 64 * 128) for b in range(2)])
+    assert torch.allclose(bpp.cpu(), bref, rtol=1e-4, atol=1e-5)
