@@ -19,9 +19,11 @@ def init_model(MODEL, quality, metric, pretrained=True):
         return codec.bmshj2018_hyperprior(quality=quality, metric=metric, pretrained=pretrained)
     if MODEL == "cheng2020":
         return codec.cheng2020_anchor(quality=quality, metric=metric, pretrained=pretrained)
-    if MODEL in ("context", "debug"):
-        raise NotImplementedError(f"model '{MODEL}' is not on this backend (out of §8 scope); "
-                                  "supported: factorized, hyper, cheng2020")
+    if MODEL == "context":
+        return codec.mbt2018(quality=quality, metric=metric, pretrained=pretrained)
+    if MODEL == "debug":
+        raise NotImplementedError("model 'debug' (ae_onelayer) is not on this backend (out of §8 scope); "
+                                  "supported: factorized, hyper, context, cheng2020")
     raise AssertionError(f"'{MODEL}' not in ['factorized', 'hyper', 'context', 'cheng2020', 'debug']")
 
 

@@ -215,6 +215,38 @@ class HyperSynthesisTransform(_ForwardOnly):
         return ex.forward(x4)
 
 
+class MbtHyperAnalysisTransform(_ForwardOnly):
+    """mbt2018 h_a = conv(M,N,3,1)-LReLU-conv(N,N,5,2)-LReLU-conv(N,N,5,2)."""
+
+    def __init__(self, N, M):
+        super().__init__(conv(M, N, stride=1, kernel_size=3), nn.LeakyReLU(inplace=True),
+                         conv(N, N, stride=2, kernel_size=5), nn.LeakyReLU(inplace=True),
+                         conv(N, N, stride=2, kernel_size=5))
+        self.out_channels = N
+
+    def _make_executor(self, sd):
+        return E.MbtHyperAnalysis(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4)
+
+
+class MbtHyperSynthesisTransform(_ForwardOnly):
+    """mbt2018 h_s = deconv(N,M)-LReLU-deconv(M,3M/2)-LReLU-conv(3M/2,2M,3,1)."""
+
+    def __init__(self, N, M):
+        super().__init__(deconv(N, M, stride=2, kernel_size=5), nn.LeakyReLU(inplace=True),
+                         deconv(M, M * 3 // 2, stride=2, kernel_size=5), nn.LeakyReLU(inplace=True),
+                         conv(M * 3 // 2, M * 2, stride=1, kernel_size=3))
+        self.out_channels = 2 * M
+
+    def _make_executor(self, sd):
+        return E.MbtHyperSynthesis(sd, prefix="")
+
+    def _run(self, ex, x4):
+        return ex.forward(x4)
+
+
 # --------------------------------------------------------------------------- #
 # cheng2020-anchor layers (compressai.layers; SURVEY §8 a17, Appendix A.7)
 # --------------------------------------------------------------------------- #
@@ -569,12 +601,38 @@ class Cheng2020Anchor(CompressionModel):
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
 
 
+class JointAutoregressiveHierarchicalPriors(CompressionModel):
+    """compressai.models.JointAutoregressiveHierarchicalPriors (mbt2018): bmshj2018 g_a / g_s, LReLU hyper
+    transforms, masked 5x5 context model.  Eval-mode forward (the attack path, anchors/model.py:95-104)."""
+    model_kind = "context"
+
+    def __init__(self, N=192, M=192, **kwargs):
+        super().__init__()
+        self.entropy_bottleneck = EntropyBottleneck(N)
+        self.g_a = AnalysisTransform(N, M)
+        self.g_s = SynthesisTransform(N, M)
+        self.h_a = MbtHyperAnalysisTransform(N, M)
+        self.h_s = MbtHyperSynthesisTransform(N, M)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.entropy_parameters = EntropyParameters(M)
+        self.context_prediction = MaskedConv2d(M, 2 * M, kernel_size=5, padding=2, stride=1)
+        self.N, self.M = int(N), int(M)
+
+    def forward(self, x):
+        if self.training:
+            raise NotImplementedError("mbt2018 training is out of scope on the HIP path (eval forward only)")
+        res = self.kernels().forward(K.to_nc4(x.detach().contiguous()))
+        return {"x_hat": K.from_nc4(res["x_hat4"], 3),
+                "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
+
+
 # --------------------------------------------------------------------------- #
 # Zoo constructors (compressai.zoo; SURVEY Appendix A.1)
 # --------------------------------------------------------------------------- #
 _CFG = {
     "bmshj2018-factorized": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
     "bmshj2018-hyperprior": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
+    "mbt2018": {q: ((192, 192) if q <= 4 else (192, 320)) for q in range(1, 9)},
     "cheng2020-anchor": {q: (128 if q <= 3 else 192, None) for q in range(1, 7)},
 }
 
@@ -612,3 +670,11 @@ def cheng2020_anchor(quality, metric="mse", pretrained=False, progress=True, **k
     N, _ = _CFG["cheng2020-anchor"][quality]
     m = Cheng2020Anchor(N)
     return _load_pretrained(m, "cheng2020-anchor", quality, metric) if pretrained else m
+
+
+def mbt2018(quality, metric="mse", pretrained=False, progress=True, **kwargs):
+    if quality not in _CFG["mbt2018"]:
+        raise ValueError(f"mbt2018 quality {quality} not in 1..8")
+    N, M = _CFG["mbt2018"][quality]
+    m = JointAutoregressiveHierarchicalPriors(N, M)
+    return _load_pretrained(m, "mbt2018", quality, metric) if pretrained else m

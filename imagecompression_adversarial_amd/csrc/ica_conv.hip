@@ -1167,7 +1167,8 @@ constexpr bool down_base() {
   if (KS == 5 && S == 2) {
     // IT = 6: the C = 192 GDN layers of bmshj2018 q6-8 (g_a forward, g_s input-gradient)
     if (IT == 6) return EPI == EPI_GDN || EPI == EPI_IGDN_BWD;
-    return gdn ? IT == 4 : (EPI == EPI_BIAS || EPI == EPI_RELU);
+    // LReLU: the mbt2018 hyper-analysis (h_a.2, CompressAI JointAutoregressiveHierarchicalPriors)
+    return gdn ? IT == 4 : (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_LRELU);
   }
   if (KS == 3 && S == 1) return gdn ? (IT == 4 || IT == 6) : true;
   if (KS == 3 && S == 2) return EPI == EPI_BIAS || EPI == EPI_LRELU;
@@ -1334,12 +1335,14 @@ static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStre
     if (it == 1) {
       if (epi == EPI_BIAS) return launch_up<5, 1, EPI_BIAS, 0>(p, st);
       if (epi == EPI_RELU) return launch_up<5, 1, EPI_RELU, 0>(p, st);
+      if (epi == EPI_LRELU) return launch_up<5, 1, EPI_LRELU, 0>(p, st);
       return -4;
     }
     if (it == 6) {  // C = 192 (bmshj2018 q6-8: g_s IGDN layers, g_a GDN input-gradients, h_s ReLU deconvs)
       switch (epi) {
         case EPI_BIAS: return launch_up<5, 6, EPI_BIAS, 0>(p, st);
         case EPI_RELU: return launch_up<5, 6, EPI_RELU, 0>(p, st);
+        case EPI_LRELU: return launch_up<5, 6, EPI_LRELU, 0>(p, st);  // mbt2018 h_s.0 (M = 192)
         case EPI_IGDN: return launch_up<5, 6, EPI_IGDN, 0>(p, st);
         case EPI_GDN_BWD: return launch_up<5, 6, EPI_GDN_BWD, 0>(p, st);
         default: return -5;
@@ -1349,6 +1352,7 @@ static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStre
       switch (epi) {
         case EPI_BIAS: return launch_up<5, 4, EPI_BIAS, 0>(p, st);
         case EPI_RELU: return launch_up<5, 4, EPI_RELU, 0>(p, st);
+        case EPI_LRELU: return launch_up<5, 4, EPI_LRELU, 0>(p, st);  // mbt2018 h_s (M = 320, 3M/2)
         case EPI_GDN: return launch_up<5, 4, EPI_GDN, 0>(p, st);
         case EPI_IGDN: return launch_up<5, 4, EPI_IGDN, 0>(p, st);
         case EPI_GDN_BWD: return launch_up<5, 4, EPI_GDN_BWD, 0>(p, st);

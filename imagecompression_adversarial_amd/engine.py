@@ -140,6 +140,53 @@ class HyperSynthesis:
         return s
 
 
+class MbtHyperAnalysis:
+    """mbt2018 h_a = conv(M,N,k3,s1)-LReLU-conv(N,N,k5,s2)-LReLU-conv(N,N,k5,s2), applied to y itself
+    (anchors/model.py:97 ``net.h_a(y)``; CompressAI JointAutoregressiveHierarchicalPriors)."""
+
+    def __init__(self, sd: dict, prefix: str = "h_a"):
+        self.M = _P(sd, prefix, "0.weight").shape[1]
+        self.N = _P(sd, prefix, "0.weight").shape[0]
+        self.convs = [K.PackedConv(_P(sd, prefix, "0.weight"), _P(sd, prefix, "0.bias"), "conv", 1),
+                      K.PackedConv(_P(sd, prefix, "2.weight"), _P(sd, prefix, "2.bias"), "conv", 2),
+                      K.PackedConv(_P(sd, prefix, "4.weight"), _P(sd, prefix, "4.bias"), "conv", 2)]
+
+    def forward(self, y4):
+        p0, p1, p2 = self.convs
+        z, _, _ = K.conv_down(y4, self.M, p0.fwd, p0.bias, self.N, 3, 1, K.EPI_LRELU)
+        z, _, _ = K.conv_down(z, self.N, p1.fwd, p1.bias, self.N, 5, 2, K.EPI_LRELU)
+        z, _, _ = K.conv_down(z, self.N, p2.fwd, p2.bias, self.N, 5, 2, K.EPI_BIAS)
+        return z
+
+
+def _up_it(C):
+    """Row tiles per wave for the k5 transposed convs (conv_up runs IT in {1, 4, 6})."""
+    return 6 if C == 192 else (1 if C <= 32 else 4)
+
+
+class MbtHyperSynthesis:
+    """mbt2018 h_s = deconv(N,M)-LReLU-deconv(M,3M/2)-LReLU-conv(3M/2,2M,k3,s1): the hyper half of the
+    (scales, means) parameters fed to entropy_parameters."""
+
+    def __init__(self, sd: dict, prefix: str = "h_s"):
+        self.N = _P(sd, prefix, "0.weight").shape[0]
+        self.M = _P(sd, prefix, "0.weight").shape[1]
+        self.M3 = _P(sd, prefix, "2.weight").shape[1]
+        self.out_channels = _P(sd, prefix, "4.weight").shape[0]
+        self.convs = [K.PackedConv(_P(sd, prefix, "0.weight"), _P(sd, prefix, "0.bias"), "deconv", 2,
+                                   it_fwd=_up_it(self.M)),
+                      K.PackedConv(_P(sd, prefix, "2.weight"), _P(sd, prefix, "2.bias"), "deconv", 2,
+                                   it_fwd=_up_it(self.M3)),
+                      K.PackedConv(_P(sd, prefix, "4.weight"), _P(sd, prefix, "4.bias"), "conv", 1)]
+
+    def forward(self, z4):
+        p0, p1, p2 = self.convs
+        s, _, _ = K.conv_up(z4, self.N, p0.fwd, p0.bias, self.M, K.EPI_LRELU, it=p0.it_fwd)
+        s, _, _ = K.conv_up(s, self.M, p1.fwd, p1.bias, self.M3, K.EPI_LRELU, it=p1.it_fwd)
+        s, _, _ = K.conv_down(s, self.M3, p2.fwd, p2.bias, self.out_channels, 3, 1, K.EPI_BIAS)
+        return s
+
+
 class CodecKernels:
     """Whole-model executor from a CompressAI-format state dict (device tensors)."""
 
@@ -159,6 +206,12 @@ class CodecKernels:
         if model == "hyper":
             self.ha = HyperAnalysis(sd)
             self.hs = HyperSynthesis(sd)
+        elif model == "context":   # mbt2018: masked 5x5 context model + 1x1 entropy_parameters stack
+            from .engine_cheng import ChengContext, ChengEntropyParameters
+            self.ha = MbtHyperAnalysis(sd)
+            self.hs = MbtHyperSynthesis(sd)
+            self.ctx = ChengContext(sd)
+            self.ep = ChengEntropyParameters(sd)
         self.eb = K.PackedEB({n: sd[f"entropy_bottleneck.{n}"] for n in K.PackedEB.NAMES})
 
     # thin aliases used by the attack loop
@@ -187,6 +240,8 @@ class CodecKernels:
             yh, ylik, ysum = K.eb_likelihood(y4, self.M, self.eb, training, noise_y4)
             xh, _ = self.gs.forward(self._to_gs(yh))
             return {"x_hat4": xh, "y4": y4, "y_hat4": yh, "lik4": {"y": ylik}, "sumlog": ysum}
+        if self.model == "context":
+            return self._forward_context(y4, training)
         z4 = self.ha.forward(y4)
         zh, zlik, zsum = K.eb_likelihood(z4, self.N, self.eb, training, noise_z4)
         s4 = self.hs.forward(zh)
@@ -194,3 +249,24 @@ class CodecKernels:
         xh, _ = self.gs.forward(self._to_gs(yh))
         return {"x_hat4": xh, "y4": y4, "y_hat4": yh, "z4": z4, "z_hat4": zh, "scales4": s4,
                 "lik4": {"y": ylik, "z": zlik}, "sumlog": ysum + zsum}
+
+    def _forward_context(self, y4, training):
+        """entropy_estimator for MODEL == "context" (anchors/model.py:95-104) + g_s(y_hat), eval mode:
+        y_hat = round(y) (quantize "dequantize", no means), params = h_s(z_hat), ctx = masked conv(y_hat),
+        (scales, means) = entropy_parameters(cat(params, ctx)).chunk(2), GC likelihood with means."""
+        if training:
+            raise NotImplementedError("mbt2018 runs eval-mode forwards only (attack path)")
+        M = self.M
+        z4 = self.ha.forward(y4)
+        zh, zlik, zsum = K.eb_likelihood(z4, self.N, self.eb, False, None)
+        params = self.hs.forward(zh)
+        y_hat4 = K.round_(y4)
+        ctx = self.ctx.forward(y_hat4)
+        gp = self.ep.forward(torch.cat((params, ctx), dim=1))   # channel concat of nChw4c tensors (M % 4 == 0)
+        c4 = (M + 3) // 4
+        scales4 = gp[:, :c4].contiguous()
+        means4 = gp[:, c4:].contiguous()
+        _, ylik, ysum = K.gc_likelihood(y4, M, scales4, means4, False, None)
+        xh, _ = self.gs.forward(self._to_gs(y_hat4))
+        return {"x_hat4": xh, "y4": y4, "y_hat4": y_hat4, "z4": z4, "z_hat4": zh, "scales4": scales4,
+                "means4": means4, "lik4": {"y": ylik, "z": zlik}, "sumlog": ysum + zsum}

@@ -17,6 +17,10 @@ Reference anchors:
     anchors/model.py:97-106): restated from the public CompressAI layer definitions (SURVEY §8 a17 and
     Appendix A.7).  CompressAI is not vendored in /root/reference and not installed, so the
     architecture itself is PARITY UNPINNED beyond its primitives (conv geometry, GDN, bounds).
+  * mbt2018 (CompressAI JointAutoregressiveHierarchicalPriors, built at anchors/model.py:74-75; composition
+    anchors/model.py:95-104, the same entropy_estimator branch as cheng2020): bmshj2018 g_a / g_s with
+    LeakyReLU hyper transforms.  Same status as cheng2020: restated from the public CompressAI definition,
+    PARITY UNPINNED beyond its primitives.
 """
 from __future__ import annotations
 
@@ -246,6 +250,8 @@ def forward(P, x, model="hyper", training=False, noise_y=None, noise_z=None):
     """net(x) -> {"x_hat", "likelihoods": {"y", "z"}} (anchors/balle.py:25-55)."""
     if model == "cheng2020":
         return cheng_forward(P, x, training, noise_y, noise_z)
+    if model == "context":
+        return mbt_forward(P, x, training, noise_y, noise_z)
     y = g_a(P, x)
     if model == "factorized":
         y_hat, y_lik = entropy_bottleneck(P, y, training, noise_y)
@@ -375,6 +381,40 @@ def cheng_forward(P, x, training=False, noise_y=None, noise_z=None):
     return {"x_hat": cheng_g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
 
 
+# --------------------------------------------------------------------------- #
+# mbt2018 (CompressAI JointAutoregressiveHierarchicalPriors)
+# --------------------------------------------------------------------------- #
+def mbt_h_a(P, y):
+    """h_a = conv3x3 s1 - LReLU - conv5x5 s2 - LReLU - conv5x5 s2 (on y, not |y|)."""
+    z = lrelu(conv(y, P["h_a.0.weight"], P["h_a.0.bias"], stride=1))
+    z = lrelu(conv(z, P["h_a.2.weight"], P["h_a.2.bias"]))
+    return conv(z, P["h_a.4.weight"], P["h_a.4.bias"])
+
+
+def mbt_h_s(P, z):
+    """h_s = deconv(N,M) - LReLU - deconv(M,3M/2) - LReLU - conv3x3 s1 (3M/2 -> 2M)."""
+    s = lrelu(deconv(z, P["h_s.0.weight"], P["h_s.0.bias"]))
+    s = lrelu(deconv(s, P["h_s.2.weight"], P["h_s.2.bias"]))
+    return conv(s, P["h_s.4.weight"], P["h_s.4.bias"], stride=1)
+
+
+def mbt_forward(P, x, training=False, noise_y=None, noise_z=None):
+    """entropy_estimator for MODEL == "context" (anchors/model.py:95-104) + g_s(y_hat) (compressor :80-84)."""
+    y = g_a(P, x)
+    z = mbt_h_a(P, y)
+    z_hat, z_lik = entropy_bottleneck(P, z, training, noise_z)
+    params = mbt_h_s(P, z_hat)
+    if training:
+        y_hat = y + (noise_y if noise_y is not None else torch.empty_like(y).uniform_(-0.5, 0.5))
+    else:
+        y_hat = torch.round(y)
+    ctx = context_prediction(P, y_hat)
+    gp = entropy_parameters(P, torch.cat((params, ctx), dim=1))
+    scales, means = gp.chunk(2, 1)
+    _, y_lik = gaussian_conditional(y, scales, means, training, noise_y)
+    return {"x_hat": g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
+
+
 def transforms(P, x, model="hyper"):
     """g_s(g_a(x)) without quantisation (the attack's expensive branch, attack_rd.py:344-349)."""
     if model == "cheng2020":
@@ -425,6 +465,17 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
     cv("g_s.4", N, N, 5, True); gd("g_s.5", N)
     cv("g_s.6", 3, N, 5, True)
     eb_ch = M if model == "factorized" else N
+    if model == "context":
+        cv("h_a.0", N, M, 3)
+        cv("h_a.2", N, N, 5)
+        cv("h_a.4", N, N, 5)
+        cv("h_s.0", M, N, 5, True)
+        cv("h_s.2", M * 3 // 2, M, 5, True)
+        cv("h_s.4", M * 2, M * 3 // 2, 3)
+        cv("context_prediction", 2 * M, M, 5)
+        cv("entropy_parameters.0", M * 10 // 3, M * 12 // 3, 1)
+        cv("entropy_parameters.2", M * 8 // 3, M * 10 // 3, 1)
+        cv("entropy_parameters.4", M * 6 // 3, M * 8 // 3, 1)
     if model == "hyper":
         cv("h_a.0", N, M, 3)
         cv("h_a.2", N, N, 5)

@@ -1,0 +1,150 @@
+"""GPU parity of the mbt2018 context model (init_model "context", anchors/model.py:74-75; its entropy
+estimator anchors/model.py:95-104): the bmshj2018 g_a / g_s at N = 192 (M = 192 for q1-4, 320 for q5-8),
+LeakyReLU hyper transforms (new conv_down k5 s2 / conv_up k5 LReLU epilogues), the masked 5x5 context
+model and the 1x1 entropy_parameters stack, against the CPU oracle (oracle/codec.py mbt_forward).
+
+Tolerances as for cheng2020 (tests/test_gpu_cheng.py): x_hat rel <= 2e-4, likelihoods rel <= 1e-3,
+bpp abs <= 1e-3.  The mbt2018 architecture is restated from public CompressAI (not vendored in the
+reference): parity unpinned beyond its primitives (oracle/codec.py header)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import attack as oa
+from oracle import codec as oc
+from tests.conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def rnd(shape, seed, lo=-1.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g) * (hi - lo) + lo
+
+
+@pytest.fixture(scope="module")
+def K():
+    from imagecompression_adversarial_amd import hip_ops
+    return hip_ops
+
+
+def _kern(q):
+    from imagecompression_adversarial_amd.engine import CodecKernels
+    P = oc.perturb_params(oc.init_params("context", q, seed=0), seed=1)
+    return P, CodecKernels({k: v.to(DEV) for k, v in P.items()}, "context")
+
+
+@pytest.fixture(scope="module")
+def mbt3():
+    return _kern(3)
+
+
+@pytest.fixture(scope="module")
+def mbt6():
+    return _kern(6)
+
+
+@pytest.mark.parametrize("KS,Cin,Cout,H,W", [(5, 192, 192, 16, 24), (5, 192, 320, 8, 12), (5, 320, 480, 8, 8)])
+def test_conv_up_lrelu(K, KS, Cin, Cout, H, W):
+    """deconv k5 s2 + LeakyReLU epilogue (h_s.0 / h_s.2), IT = 6 for 192 outputs, 4 otherwise."""
+    from imagecompression_adversarial_amd.engine import _up_it
+    w = rnd((Cin, Cout, KS, KS), 40, -0.05, 0.05)
+    b = rnd((Cout,), 41, -0.1, 0.1)
+    x = rnd((2, Cin, H, W), 42)
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "deconv", 2, it_fwd=_up_it(Cout))
+    y4, _, _ = K.conv_up(K.to_nc4(x.to(DEV)), Cin, p.fwd, p.bias, Cout, K.EPI_LRELU, it=p.it_fwd)
+    ref = F.leaky_relu(F.conv_transpose2d(x, w, b, stride=2, padding=2, output_padding=1), 0.01)
+    assert rel_err(K.from_nc4(y4, Cout).cpu(), ref) < 1e-4
+
+
+def test_conv_down_k5s2_lrelu(K):
+    """conv k5 s2 + LeakyReLU epilogue (h_a.2)."""
+    w = rnd((192, 192, 5, 5), 43, -0.05, 0.05)
+    b = rnd((192,), 44, -0.1, 0.1)
+    x = rnd((2, 192, 32, 48), 45)
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2)
+    y4, _, _ = K.conv_down(K.to_nc4(x.to(DEV)), 192, p.fwd, p.bias, 192, 5, 2, K.EPI_LRELU)
+    ref = F.leaky_relu(F.conv2d(x, w, b, stride=2, padding=2), 0.01)
+    assert rel_err(K.from_nc4(y4, 192).cpu(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("which", ["mbt3", "mbt6"])
+def test_mbt_eval_forward_vs_oracle(K, which, request):
+    P, kern = request.getfixturevalue(which)
+    M = kern.M
+    x = rnd((2, 3, 128, 192), 46, 0.0, 1.0)
+    res = kern.forward(K.to_nc4(x.to(DEV)))
+    ref = oc.forward(P, x, "context")
+    assert rel_err(K.from_nc4(res["x_hat4"], 3).cpu(), ref["x_hat"]) < 2e-4
+    assert rel_err(K.from_nc4(res["lik4"]["y"], M).cpu(), ref["likelihoods"]["y"]) < 1e-3
+    assert rel_err(K.from_nc4(res["lik4"]["z"], 192).cpu(), ref["likelihoods"]["z"]) < 1e-3
+    bpp = K.bits_to_bpp(res["sumlog"], 128 * 192).cpu()
+    bref = torch.stack([oc.bpp({k: v[b:b + 1] for k, v in ref["likelihoods"].items()}, 128 * 192)
+                        for b in range(2)])
+    assert torch.allclose(bpp, bref, rtol=0, atol=1e-3)
+
+
+def test_mbt_transforms_fwd_dgrad_vs_oracle(K, mbt3):
+    P, kern = mbt3
+    x = rnd((2, 3, 128, 128), 47, 0.0, 1.0)
+    y4, sa = kern.g_a(K.to_nc4(x.to(DEV)), save=True)
+    xh4, ss = kern.g_s(y4, save=True)
+    xr = x.clone().requires_grad_(True)
+    yr = oc.g_a(P, xr)
+    xhr = oc.g_s(P, yr)
+    assert rel_err(K.from_nc4(y4, 192).cpu(), yr.detach()) < 2e-4
+    assert rel_err(K.from_nc4(xh4, 3).cpu(), xhr.detach()) < 2e-4
+    gout = rnd(xhr.shape, 48)
+    xhr.backward(gout)
+    gy4 = kern.g_s_backward(K.to_nc4(gout.to(DEV)), ss)
+    gx4 = kern.g_a_backward(gy4, sa)
+    assert rel_err(K.from_nc4(gx4, 3).cpu(), xr.grad) < 1e-3
+
+
+def test_mbt_model_dropin(mbt3):
+    """init_model("context") -> JointAutoregressiveHierarchicalPriors: state-dict names, net(x), compressor and
+    the standalone h_a / h_s / context_prediction / entropy_parameters modules."""
+    from imagecompression_adversarial_amd.anchors import model as am
+    P, _ = mbt3
+    net = am.init_model("context", 3, "mse", pretrained=False)
+    sd = net.state_dict()
+    missing = [k for k in P if k not in sd]
+    assert not missing, missing[:5]
+    sd.update({k: v.reshape(sd[k].shape) for k, v in P.items()})
+    net.load_state_dict(sd)
+    net = net.to(DEV).eval()
+    x = rnd((1, 3, 128, 128), 49, 0.0, 1.0)
+    with torch.no_grad():
+        out = net(x.to(DEV))
+        comp = am.compressor(x.to(DEV), net, "context")
+        z = net.h_a(net.g_a(x.to(DEV)))
+    ref = oc.forward(P, x, "context")
+    assert rel_err(out["x_hat"].cpu(), ref["x_hat"]) < 2e-4
+    assert rel_err(comp["x_hat"].cpu(), ref["x_hat"]) < 2e-4
+    for k in ("y", "z"):
+        assert rel_err(comp["likelihoods"][k].cpu(), ref["likelihoods"][k]) < 1e-3
+    assert rel_err(z.cpu(), oc.mbt_h_a(P, oc.g_a(P, x))) < 2e-4
+
+
+def test_mbt_attack_vs_oracle(mbt3):
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = mbt3
+    x = rnd((2, 3, 64, 64), 50, 0.0, 1.0)
+    res = attack_batch(kern, x.to(DEV), steps=4, noise_thr=1e-5, eval_msssim=False, record=True)
+    rec = []
+    ref = oa.attack(P, x, steps=4, noise_thr=1e-5, model="context", eval_msssim=False, record=rec)
+    for i, br in enumerate(res.branches):
+        assert [bool(v) for v in br] == [bool(v) for v in rec[i]["cheap"]], i
+    assert rel_err(res.noise.cpu(), ref.noise) < 2e-3
+    assert rel_err(res.output_s.cpu(), ref.output_s) < 2e-4
+
+
+def test_mbt_cli_runs(capsys):
+    from imagecompression_adversarial_amd import attack_rd, coder
+    args = coder.config().parse_args(["-m", "context", "-metric", "mse", "-q", "5", "-steps", "2",
+                                      "-s", "synthetic:2x128x192", "--synthetic-weights", "--batch", "2"])
+    out = attack_rd.main(args)
+    txt = capsys.readouterr().out
+    assert "AVG: context-mse-5" in txt
+    assert out["bpp_ori"] > 0
