@@ -61,6 +61,10 @@ _SIGS = {
     "ica_flip_rot": [_p, _p, _l, _i, _i, _i, _p],
     "ica_bitdepth": [_p, _p, _l, _f, _p],
     "ica_resample_axis": [_p, _p, _l, _i, _i, _i, _i, _p, _p, _p, _i, _p],
+    "ica_bitdepth_noise": [_p, _p, _p, _l, _f, _p],
+    "ica_bitdepth_noise_bwd": [_p, _p, _l, _f, _p],
+    "ica_add": [_p, _p, _p, _l, _p],
+    "ica_ensemble_grad": [_p, _p, _p, _l, _f, _p],
     "ica_round": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],

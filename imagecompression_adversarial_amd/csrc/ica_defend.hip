@@ -73,6 +73,37 @@ __global__ void resample_axis_kernel(const float* __restrict__ x, float* __restr
   }
 }
 
+// --adv (attacking through the defence, self_ensemble.py:253-268): the training-mode inputs of defend().
+// bitdepth_reduction(x, inference=False) (:66-69): y = (x * scale + u) / scale, u ~ U(-0.5, 0.5) given;
+// its autograd input gradient is (g / scale) * scale (div then mul backward, fp32 as torch computes it).
+__global__ void bitdepth_noise_kernel(const float* __restrict__ x, const float* __restrict__ u, float* __restrict__ y,
+                                      long n, float scale) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = __fdiv_rn(__fadd_rn(__fmul_rn(x[i], scale), u[i]), scale);
+}
+__global__ void bitdepth_noise_bwd_kernel(const float* __restrict__ g, float* __restrict__ gx, long n, float scale) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    gx[i] = __fmul_rn(__fdiv_rn(g[i], scale), scale);
+}
+// y = a + b (the "noise" quantisation y_hat = y + u of a training-mode forward)
+__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = __fadd_rn(a[i], b[i]);
+}
+// Loss gradient of the self-ensemble branch (self_ensemble.py:112, :261-270): output_ = clamp(o, 0, 1) with o the
+// best variant's reconstruction rotated back; loss_o = 1 - mean((out_s - output_)^2) per image ->
+// d loss_o / d o = 2 invN (out_s - output_) where 0 <= o <= 1 (torch.clamp backward), else 0.  The Up/Low
+// bounds applied on top with --clamp are identities on [0, 1] values and pass the gradient.
+__global__ void ensemble_grad_kernel(const float* __restrict__ o, const float* __restrict__ out_s,
+                                     float* __restrict__ g, long n, float invN) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = o[i];
+    const float c = fminf(fmaxf(v, 0.f), 1.f);
+    const float t = __fmul_rn(invN, __fsub_rn(out_s[i], c));
+    g[i] = (v >= 0.f && v <= 1.f) ? __fadd_rn(t, t) : 0.f;
+  }
+}
+
 static inline int grid_1d_def(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
@@ -99,6 +130,30 @@ int ica_resample_axis(const float* x, float* y, long planes, int H, int W, int a
   const long total = planes * (axis == 0 ? (long)out_len * W : (long)H * out_len);
   hipLaunchKernelGGL(resample_axis_kernel, dim3(grid_1d_def(total)), dim3(256), 0, st, x, y, planes, H, W, axis,
                      out_len, xmin, xsize, w, K);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_bitdepth_noise(const float* x, const float* u, float* y, long n, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(bitdepth_noise_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, x, u, y, n, scale);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_bitdepth_noise_bwd(const float* g, float* gx, long n, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(bitdepth_noise_bwd_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, g, gx, n, scale);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_add(const float* a, const float* b, float* y, long n, hipStream_t st) {
+  hipLaunchKernelGGL(add_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, a, b, y, n);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_ensemble_grad(const float* o, const float* out_s, float* g, long n, float invN, hipStream_t st) {
+  hipLaunchKernelGGL(ensemble_grad_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, o, out_s, g, n, invN);
   ICA_CHECK_LAUNCH();
   return 0;
 }

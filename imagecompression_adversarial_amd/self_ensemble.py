@@ -11,6 +11,7 @@ self_ensemble       self_ensemble.py:85-131  best of the 8 variants by mse(varia
 defend              self_ensemble.py:156-171
 evaluate_defend     self_ensemble.py:173-252 (eval with args.defend)
 attack_/main        self_ensemble.py:275-444 (the L2 attack loop == attack.attack_batch, then eval with defend)
+DefendedAttackLoop  self_ensemble.py:253-326 with --adv: the attack through defend() (ensemble / bitdepth / resize)
 
 Reference semantics kept as they are (SURVEY Appendix B style):
   * ensemble: eval re-runs net(best_x) and compares its reconstruction, in the transformed frame of the
@@ -34,7 +35,7 @@ from . import coder
 from . import hip_ops as K
 from . import msssim as MS
 from ._lib import call, ptr, stream
-from .attack import attack_batch, eval_forward
+from .attack import AttackLoop, attack_batch, eval_forward, evaluate
 
 RESIZE_SCALE = 243.0 / 256.0  # self_ensemble.py:160 random_resize(x, scale=243/256, random=False)
 
@@ -256,12 +257,202 @@ def evaluate_defend(kern, im_adv, im_s, output_s, method="ensemble", clamp=True,
 
 
 # --------------------------------------------------------------------------- #
+# Attacking through the defence (--adv; self_ensemble.py:253-326)
+# --------------------------------------------------------------------------- #
+BITDEPTH_SCALE = float(2 ** 6 - 1)   # bitdepth_reduction(bits=6)
+
+
+def variant(x, i):
+    """rotates(x)[i] alone (the forward transform of dihedral variant i)."""
+    if i == 0:
+        return x
+    if i in (1, 2, 3):
+        t = _flip_rot(x, FLIP_H) if i != 2 else _flip_rot(x, FLIP_W)
+        return _flip_rot(t, FLIP_W) if i == 3 else t
+    r = _flip_rot(x, ROT_P)
+    if i == 4:
+        return r
+    t = _flip_rot(r, FLIP_H) if i != 6 else _flip_rot(r, FLIP_W)
+    return _flip_rot(t, FLIP_W) if i == 7 else t
+
+
+def aa_table_t(tab, in_size: int):
+    """Transpose of one resample pass (its input gradient) as a gather table over the pass's outputs: for input
+    index i the outputs whose support holds i form one contiguous range (xmin, xsize nondecreasing)."""
+    xmin, xsize, wt = tab
+    rows = [[] for _ in range(in_size)]
+    for o in range(len(xmin)):
+        for k in range(int(xsize[o])):
+            rows[int(xmin[o]) + k].append((o, wt[o, k]))
+    Kt = max(1, max(len(r) for r in rows))
+    xm = np.zeros(in_size, np.int32)
+    xs = np.zeros(in_size, np.int32)
+    w = np.zeros((in_size, Kt), np.float32)
+    for i, r in enumerate(rows):
+        if r:
+            os_ = [o for o, _ in r]
+            if os_ != list(range(os_[0], os_[0] + len(os_))):
+                raise AssertionError("resample support is not contiguous")
+            xm[i], xs[i] = os_[0], len(os_)
+            w[i, :len(r)] = [v for _, v in r]
+    return xm, xs, w
+
+
+class _ResizePair:
+    """random_resize(x, 243/256) as four separable passes plus their transposes (input gradient)."""
+
+    def __init__(self, H, W, scale=RESIZE_SCALE):
+        Ho, Wo = math.floor(H * scale), math.floor(W * scale)
+        H2, W2 = math.floor(Ho / scale), math.floor(Wo / scale)
+        if (H2, W2) != (H, W):
+            raise RuntimeError(f"resize {H}x{W} -> {Ho}x{Wo} -> {H2}x{W2} changes the image size (the reference's "
+                               "loss against output_s fails the same way)")
+        self.fw = [(1, Wo, aa_table(W, Wo, scale)), (0, Ho, aa_table(H, Ho, scale)),
+                   (1, W, aa_table(Wo, W, 1.0 / scale)), (0, H, aa_table(Ho, H, 1.0 / scale))]
+        ins = [W, H, Wo, Ho]
+        self.bw = [(ax, n_in, aa_table_t(tab, n_in)) for (ax, _, tab), n_in in zip(self.fw, ins)][::-1]
+
+    def forward(self, x):
+        for ax, n, tab in self.fw:
+            x = _resample(x, ax, n, tab)
+        return x
+
+    def backward(self, g):
+        for ax, n, tab in self.bw:
+            g = _resample(g, ax, n, tab)
+        return g
+
+
+def _select(saved, rows):
+    """index_select every tensor of a saved-activation structure along the batch dimension."""
+    if saved is None:
+        return None
+    if isinstance(saved, torch.Tensor):
+        return saved.index_select(0, rows)
+    return type(saved)(_select(s, rows) for s in saved)
+
+
+class DefendedAttackLoop(AttackLoop):
+    """self_ensemble.attack_ with args.adv: the expensive branch encodes defend(net, im_in, method) in training
+    mode (self_ensemble.py:259-262) and the loss gradient flows back through the defence:
+      ensemble : all 8 dihedral variants through g_s(g_a(.)) (two cat-of-4 batches, :85-131); the variant with
+                 the least mse(variant, reconstruction) (first minimum) carries the gradient:
+                 output_ = clamp(rotate_back(x_hat_best)) -> torch.clamp mask -> variant transform -> g_s/g_a
+                 input gradient -> inverse transform.
+      bitdepth : x_ = (x * 63 + u) / 63, x_hat = g_s(g_a(x_) + u_y) (net(x_) in training mode: y_hat = y + noise
+                 for every model), the usual bounded L2 output loss.
+      resize   : x_ = up(down(x)) (antialiased bicubic 243/256), x_hat = g_s(g_a(x_) + u_y); gradient through the
+                 transposed resample passes.
+    noise_fn(step, name, shape) may supply the uniform draws ("x": bit-depth noise, "y": latent noise); default:
+    torch's device generator, U(-0.5, 0.5) as the reference draws them."""
+
+    def __init__(self, kern, im_s, method="ensemble", noise_fn=None, **kw):
+        if method not in ("ensemble", "resize", "bitdepth"):
+            raise ValueError(f"{method} not in 'ensemble', 'resize', 'bitdepth'")
+        if kw.get("att_metric", "L2") != "L2" or kw.get("target") is not None or kw.get("coupled"):
+            raise NotImplementedError("self_ensemble's attack is the per-image L2 attack")
+        super().__init__(kern, im_s, **kw)
+        self.method, self.noise_fn = method, noise_fn
+        self.resize = _ResizePair(self.H, self.W) if method == "resize" else None
+        self.best_hist = []   # per step: the best variant index of each image (ensemble)
+
+    def _uniform(self, name, shape, i):
+        if self.noise_fn is not None:
+            return self.noise_fn(i, name, shape).to(self.im_s.device, torch.float32).contiguous()
+        return torch.empty(shape, device=self.im_s.device).uniform_(-0.5, 0.5)
+
+    def step(self, i, record_im_in=False, census=False):
+        self._i = i
+        return super().step(i, record_im_in, census)
+
+    def network_grad(self):
+        if self.method == "ensemble":
+            return self._grad_ensemble()
+        return self._grad_noisy()
+
+    def _grad_noisy(self):
+        kern, B, H, W = self.kern, self.B, self.H, self.W
+        x = K.from_nc4(self.im_in4, 3)
+        if self.method == "bitdepth":
+            u = self._uniform("x", x.shape, self._i)
+            xp = torch.empty_like(x)
+            call("ica_bitdepth_noise", ptr(x), ptr(u), ptr(xp), x.numel(), BITDEPTH_SCALE, stream())
+        else:
+            xp = self.resize.forward(x)
+        y4, sa = kern.g_a(K.to_nc4(xp), save=True)
+        uy = self._uniform("y", (B, kern.M, y4.shape[2], y4.shape[3]), self._i)
+        yh4 = torch.empty_like(y4)
+        call("ica_add", ptr(y4), ptr(K.to_nc4(uy)), ptr(yh4), y4.numel(), stream())
+        del y4
+        xh4, ss = kern.g_s(yh4, save=True)
+        call("ica_attack_loss", ptr(xh4), ptr(self.output_s), ptr(self.grad4), ptr(self.part), B, H, W,
+             self.gscale, int(self.clamp), 0, stream())
+        g = K.from_nc4(kern.g_a_backward(kern.g_s_backward(self.grad4, ss), sa), 3)
+        if self.method == "bitdepth":
+            gx = torch.empty_like(g)
+            call("ica_bitdepth_noise_bwd", ptr(g), ptr(gx), g.numel(), BITDEPTH_SCALE, stream())
+        else:
+            gx = self.resize.backward(g)
+        return K.to_nc4(gx)
+
+    def _grad_ensemble(self):
+        kern, B = self.kern, self.B
+        x = K.from_nc4(self.im_in4, 3)
+        xs = rotates(x)
+        groups, mses = [], []
+        for grp in (xs[:4], xs[4:]):
+            xcat = torch.cat(grp, dim=0)                     # variant-major, as cat(xs[:4]) per image
+            y4, sa = kern.g_a(K.to_nc4(xcat), save=True)
+            xh4, ss = kern.g_s(y4, save=True)
+            del y4
+            xh = K.from_nc4(xh4, 3)
+            mses.append(K.sqdiff_mean(xcat, xh).view(4, B))
+            groups.append((xh, sa, ss))
+        best = torch.argmin(torch.cat(mses, 0), dim=0).tolist()   # first minimum, like the strict '<' scan
+        self.best_hist.append(best)
+        gx = torch.empty_like(x)
+        for gi, (xh, sa, ss) in enumerate(groups):
+            imgs = [b for b in range(B) if best[b] // 4 == gi]
+            if not imgs:
+                continue
+            rows = torch.tensor([(best[b] % 4) * B + b for b in imgs], device=x.device)
+            gv = []
+            for b in imgs:
+                o = rotates(xh[(best[b] % 4) * B + b:(best[b] % 4) * B + b + 1], reverse=best[b]).contiguous()
+                g = torch.empty_like(o)
+                call("ica_ensemble_grad", ptr(o), ptr(self.output_s[b:b + 1]), ptr(g), o.numel(), self.gscale,
+                     stream())
+                gv.append(variant(g, best[b]))
+            g4 = K.to_nc4(torch.cat(gv, 0))
+            gxv = K.from_nc4(kern.g_a_backward(kern.g_s_backward(g4, _select(ss, rows)), _select(sa, rows)), 3)
+            for j, b in enumerate(imgs):
+                gx[b:b + 1] = rotates(gxv[j:j + 1].contiguous(), reverse=best[b])
+        return K.to_nc4(gx)
+
+
+def adv_attack_batch(kern, im_s, method="ensemble", steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, clamp=True,
+                     noise_fn=None, defend_eval=False, eval_msssim=True, record=False):
+    """self_ensemble.attack_ with --adv (per image), then its eval (with --defend when defend_eval).
+    Returns (AttackResult-like dict of the eval, the loop)."""
+    loop = DefendedAttackLoop(kern, im_s, method, noise_fn, steps=steps, epsilon=epsilon, noise_thr=noise_thr,
+                              lr=lr, clamp=clamp)
+    branches = loop.run(record=record)
+    if defend_eval:
+        res, out = evaluate_defend(kern, loop.im_in, loop.im_s, loop.output_s, method, clamp, adv=True,
+                                   msssim=eval_msssim)
+    else:
+        im_, out, bpp, mse_in, mse_out, msim_in, msim_out, vi, vi_msim = evaluate(
+            kern, loop.im_in, loop.im_s, loop.output_s, clamp, adv=True, msssim=eval_msssim)
+        res = [{"bpp": float(bpp[b]), "mse_in": float(mse_in[b]), "mse_out": float(mse_out[b]), "vi": vi[b],
+                "vi_msim": vi_msim[b]} for b in range(loop.B)]
+    return res, out, loop, branches
+
+
+# --------------------------------------------------------------------------- #
 # CLI (self_ensemble.py:317-444): attack, then the defended eval
 # --------------------------------------------------------------------------- #
 def batch_attack(args):
     from .attack_rd import _sources
-    if args.adv:
-        raise NotImplementedError("attacking through the self-ensemble (--adv) is not supported")
     print("==================== ATTACK SETTINGS ====================")
     print("[ IMAGE ]:", args.source, "->", args.target)
     print("Attack Loss Metric:", args.att_metric)
@@ -281,6 +472,21 @@ def batch_attack(args):
     for name, t, _, _ in _sources(args.source):
         start = time.time()
         im_s = (t if t is not None else coder.read_image(name)[0]).to(args.device)
+        if args.adv:   # attack through defend(net, im_in, args.method) (self_ensemble.py:259-262)
+            rs, _, loop, _ = adv_attack_batch(kern, im_s, args.method, steps=args.steps, epsilon=args.epsilon,
+                                              noise_thr=args.noise, lr=args.lr_attack, clamp=args.clamp,
+                                              defend_eval=args.defend, eval_msssim=min(im_s.shape[2:]) > 160)
+            r = rs[0]
+            bpp, vi = r["bpp"], r["vi"]
+            if args.defend and pre:
+                vi_pre_ += r["vi_pre"] if r["vi_pre"] is not None else 0.0
+            bpp_ori = float(loop.bpp_ori[0])
+            print(name, bpp_ori, bpp, vi, "Time:", time.time() - start)
+            bpp_ori_ += bpp_ori
+            bpp_ += bpp
+            vi_ += vi if vi is not None else 0.0
+            n += 1
+            continue
         res = attack_batch(kern, im_s, steps=args.steps, epsilon=args.epsilon, noise_thr=args.noise,
                            lr=args.lr_attack, clamp=args.clamp, eval_msssim=False)
         if args.defend:

@@ -87,6 +87,14 @@ int ica_bitdepth(const float* x, float* y, long n, float scale, hipStream_t stre
  * the tables are device arrays built on the host (self_ensemble.aa_table). */
 int ica_resample_axis(const float* x, float* y, long planes, int H, int W, int axis, int out_len, const int* xmin,
                       const int* xsize, const float* w, int K, hipStream_t stream);
+/* Attacking through the defence (self_ensemble.py --adv, :253-270):
+ * y = (x * scale + u) / scale (bitdepth_reduction(inference=False), :66-69, u given) and its input gradient
+ * gx = (g / scale) * scale; y = a + b (training-mode "noise" quantisation of the latent);
+ * ensemble branch loss gradient g = [0 <= o <= 1] * 2 invN (out_s - clamp(o, 0, 1)) (:112, :261-270). */
+int ica_bitdepth_noise(const float* x, const float* u, float* y, long n, float scale, hipStream_t stream);
+int ica_bitdepth_noise_bwd(const float* g, float* gx, long n, float scale, hipStream_t stream);
+int ica_add(const float* a, const float* b, float* y, long n, hipStream_t stream);
+int ica_ensemble_grad(const float* o, const float* out_s, float* g, long n, float invN, hipStream_t stream);
 /* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
  * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
  * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,

@@ -90,13 +90,16 @@ def _masked_mean(e, m):
 
 def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
            clamp=True, model="hyper", coupled=False, init_noise=None, eval_msssim=True,
-           record=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0):
+           record=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0, expensive=None,
+           adv=False):
     """attack_rd.attack_ restated (Adam on additive noise, L-inf box in the forward).
 
     record: optional list; per step appends dict(loss_i, branch) for trajectory tests.
     target / roi: the targeted / ROI attack (SURVEY §8f rank 1, semantics as DESIGN.md states them;
     the reference's own masked loss (attack_data.py:219-221) multiplies scalar means by mask tensors, so
     its masked means are restated here as proper per-region means):
+    expensive: optional f(im_in_subset, step) -> x_ replacing g_s(g_a(.)) in the expensive branch (the --adv
+    attack through a defence, oracle.defend.adv_*); adv: the eval's args.adv (no vi_msim).
       loss_i = mean_tar((s - ii)^2) + la_bkg_in * mean_bkg((s - ii)^2)
       loss_o = la_tar * mean_tar((out_t - o)^2) + la_bkg_out * mean_bkg((out_s - o)^2)   (minimised)
     """
@@ -143,7 +146,7 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
                 raise ValueError(att_metric)
         if bool((~cheap).any()):
             idx = (~cheap).nonzero().flatten()
-            x_ = codec.transforms(P, im_in[idx], model)
+            x_ = codec.transforms(P, im_in[idx], model) if expensive is None else expensive(im_in[idx], i)
             out = codec.bound01(x_) if clamp else x_
             if att_metric == "L2":
                 if coupled:
@@ -165,7 +168,7 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
         if i % max(steps // 3, 1) == 0:
             sch.step()
     im_in = im_in.detach()
-    ev = eval_batch(P, im_in, im_s, output_s, model, clamp, adv=False, msssim=eval_msssim)
+    ev = eval_batch(P, im_in, im_s, output_s, model, clamp, adv=adv, msssim=eval_msssim)
     return SimpleNamespace(im_adv=ev.im, output_adv=ev.out, output_s=output_s, bpp_ori=bpp_ori,
                            bpp=ev.bpp, eval=ev, noise=noise.detach(), im_in=im_in)
 

@@ -7,6 +7,8 @@ F.interpolate(mode="bicubic", antialias=True)) restated; self_ensemble.py itself
 
   * ``self_ensemble``  self_ensemble.py:85-131, per image (the reference runs B = 1)
   * ``eval_defend``    self_ensemble.eval with args.defend (self_ensemble.py:173-252)
+  * ``adv_expensive``  the --adv expensive branch (self_ensemble.py:259-262): x_ of defend(net, im_in) in
+                       training mode, differentiable, for oracle.attack.attack(expensive=...)
 """
 from __future__ import annotations
 
@@ -115,3 +117,40 @@ def eval_defend(P, im_adv, im_s, output_s, method="ensemble", model="hyper", cla
                     r["vi_msim"] = 10.0 * math.log10((1 - float(msim_out[b])) / (1 - float(msim_in[b])))
             results.append(r)
     return results, output_
+
+
+def adv_expensive(P, method="ensemble", noise_fn=None, model="hyper", chosen=None):
+    """f(im_in, step) -> x_ of defend(net, im_in, method) with net.training (self_ensemble.py:85-131, :156-171):
+      ensemble : per image, g_s(g_a(.)) of the variants as two cat-of-4 batches, the first least
+                 mean((x_v - x_hat_v)^2) wins, x_ = clamp(rotates(x_hat_best, reverse=best), 0, 1)
+      bitdepth : x_ = g_s(g_a((x * 63 + u) / 63) + u_y)     (net(x_)["x_hat"] in training mode)
+      resize   : x_ = g_s(g_a(random_resize(x, 243/256)) + u_y)
+    noise_fn(step, name, shape) supplies the U(-0.5, 0.5) draws ("x", "y"); chosen (list) records best
+    indices per call."""
+    def f(x, step):
+        if method == "ensemble":
+            outs, picks = [], []
+            for b in range(x.shape[0]):
+                xs = rotates(x[b:b + 1])
+                best = (float("inf"), 0, None)
+                for grp, base in ((xs[:4], 0), (xs[4:], 4)):
+                    xh = codec.transforms(P, torch.cat(grp, 0), model)
+                    for j in range(4):
+                        m = torch.mean((grp[j] - xh[j:j + 1]) ** 2)
+                        if m < best[0]:
+                            best = (m, base + j, xh[j:j + 1])
+                picks.append(best[1])
+                outs.append(torch.clamp(rotates(best[2], reverse=best[1]), 0.0, 1.0))
+            if chosen is not None:
+                chosen.append(picks)
+            return torch.cat(outs, 0)
+        if method == "bitdepth":
+            scale = 2 ** 6 - 1
+            xp = (x * scale + noise_fn(step, "x", tuple(x.shape))) / scale
+        elif method == "resize":
+            xp = random_resize(x, 243 / 256)
+        else:
+            raise ValueError(method)
+        y = codec.g_a(P, xp)
+        return codec.g_s(P, y + noise_fn(step, "y", tuple(y.shape)))
+    return f
