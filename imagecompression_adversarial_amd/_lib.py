@@ -65,6 +65,12 @@ _SIGS = {
     "ica_bitdepth_noise_bwd": [_p, _p, _l, _f, _p],
     "ica_add": [_p, _p, _p, _l, _p],
     "ica_ensemble_grad": [_p, _p, _p, _l, _f, _p],
+    "ica_gc_symbols": [_p, _p, _p, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p],
+    "ica_eb_symbols": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_dequantize": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_pmf_to_quantized_cdf": [_p, _i, _i, _p],
+    "ica_rans_encode": [_p, _p, _l, _p, _i, _p, _p, _i, _p, _l, _p],
+    "ica_rans_decode": [_p, _l, _p, _l, _p, _i, _p, _p, _i, _p],
     "ica_round": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],
@@ -92,7 +98,8 @@ _SIGS = {
     "ica_eb_param_scatter": [_p, _p, _p, _i, _p],
     "ica_mse_grad": [_p, _p, _p, _i, _i, _i, _f, _p],
 }
-_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_conv_weight_bf16_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz}
+_RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_conv_weight_bf16_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz,
+             "ica_rans_encode": _l}
 
 
 

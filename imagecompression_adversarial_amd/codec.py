@@ -399,6 +399,23 @@ class EntropyModel(nn.Module):
         self.register_buffer("_quantized_cdf", torch.IntTensor())
         self.register_buffer("_cdf_length", torch.IntTensor())
 
+    def _coder_tables(self):
+        """Host coding tables from the `_quantized_cdf` / `_cdf_length` / `_offset` buffers (cached)."""
+        from . import entropy_coding as EC_
+        if self._offset.numel() == 0:
+            raise ValueError("Entropy model is not updated: run update() first (CompressAI semantics)")
+        k = tuple((b.data_ptr(), b._version) for b in (self._quantized_cdf, self._cdf_length, self._offset))
+        if getattr(self, "_tab_key", None) != k:
+            self._tab = EC_.Tables(self._quantized_cdf, self._cdf_length, self._offset)
+            self._tab_key = k
+        return self._tab
+
+    def _set_tables(self, cdf, length, offset):
+        dev = self._offset.device
+        self._quantized_cdf = cdf.to(dev)
+        self._cdf_length = length.to(dev)
+        self._offset = offset.to(dev)
+
     def quantize(self, inputs, mode, means=None):
         """CompressAI EntropyModel.quantize ("noise" | "dequantize" | "symbols"); round = half-to-even."""
         if mode not in ("noise", "dequantize", "symbols"):
@@ -470,6 +487,35 @@ class EntropyBottleneck(EntropyModel):
     def _get_medians(self):
         return self.quantiles[:, :, 1:2]
 
+    def update(self, force: bool = False) -> bool:
+        """EntropyBottleneck.update: the quantised CDF tables (entropy_coding.eb_tables)."""
+        from . import entropy_coding as EC_
+        if self._offset.numel() > 0 and not force:
+            return False
+        prm = {n: getattr(self, n) for n in K.PackedEB.NAMES if not n.startswith("quantiles")}
+        self._set_tables(*EC_.eb_tables(prm, self.quantiles, len(self.filters)))
+        return True
+
+    def compress(self, x):
+        """x [B, C, H, W] on the HIP device -> one rANS bitstream per image (symbols round(x - median))."""
+        from . import entropy_coding as EC_
+        tab = self._coder_tables()
+        B, C, H, W = x.shape
+        sym, idx = EC_.eb_symbols(K.to_nc4(x.detach().contiguous()), C, self._get_medians().detach().reshape(-1)
+                                  .contiguous())
+        return EC_.encode_batch(sym, idx, tab)
+
+    def decompress(self, strings, size):
+        from . import entropy_coding as EC_
+        tab = self._coder_tables()
+        H, W = int(size[0]), int(size[1])
+        B, C = len(strings), self.channels
+        dev = self.quantiles.device
+        idx = EC_.eb_indexes(B, C, H, W, "cpu")
+        sym = EC_.decode_batch(strings, idx, tab)
+        med = self._get_medians().detach().reshape(-1).contiguous()
+        return K.from_nc4(EC_.dequantize(sym, B, C, H, W, medians=med, device=dev), C)
+
     def forward(self, x, training=None):
         if training is None:
             training = self.training
@@ -488,6 +534,46 @@ class GaussianConditional(EntropyModel):
         self.register_buffer("scale_table", torch.Tensor(tuple(scale_table) if scale_table else ()))
         self.register_buffer("scale_bound", torch.Tensor([float(scale_bound)]))
         self.lower_bound_scale = LowerBound(scale_bound)
+
+    def update_scale_table(self, scale_table, force: bool = False) -> bool:
+        if self._offset.numel() > 0 and not force:
+            return False
+        dev = self.scale_bound.device
+        self.scale_table = torch.Tensor(tuple(float(v) for v in scale_table)).to(dev)
+        self.update()
+        return True
+
+    def update(self):
+        """GaussianConditional.update: one quantised CDF per scale_table entry (entropy_coding.gc_tables)."""
+        from . import entropy_coding as EC_
+        self._set_tables(*EC_.gc_tables(self.scale_table, self.tail_mass))
+
+    def build_indexes(self, scales):
+        from . import entropy_coding as EC_
+        s4 = K.to_nc4(scales.detach().contiguous())
+        B, C, H, W = scales.shape
+        _, idx = EC_.gc_symbols(s4, C, s4, None, self.scale_table.to(scales.device).contiguous(),
+                                float(self.scale_bound))
+        return idx.view(B, C, H, W)
+
+    def compress(self, inputs, indexes, means=None):
+        from . import entropy_coding as EC_
+        tab = self._coder_tables()
+        B, C, H, W = inputs.shape
+        y4 = K.to_nc4(inputs.detach().contiguous())
+        m4 = K.to_nc4(means.detach().contiguous()) if means is not None else None
+        sym, _ = EC_.gc_symbols(y4, C, y4, m4, self.scale_table.to(inputs.device).contiguous(),
+                                float(self.scale_bound))
+        return EC_.encode_batch(sym, indexes.reshape(B, -1).to(torch.int32), tab)
+
+    def decompress(self, strings, indexes, dtype=torch.float, means=None):
+        from . import entropy_coding as EC_
+        tab = self._coder_tables()
+        B, C, H, W = indexes.shape
+        sym = EC_.decode_batch(strings, indexes.reshape(B, -1).to(torch.int32), tab)
+        dev = indexes.device if indexes.is_cuda else self.scale_bound.device
+        m4 = K.to_nc4(means.detach().contiguous()) if means is not None else None
+        return K.from_nc4(EC_.dequantize(sym, B, C, H, W, means4=m4, device=dev), C).to(dtype)
 
     def forward(self, inputs, scales, means=None, training=None):
         if training is None:
@@ -518,6 +604,19 @@ class CompressionModel(nn.Module):
                     if key in state_dict and hasattr(mod, b):
                         getattr(mod, b).resize_(state_dict[key].size())
         return super().load_state_dict(state_dict, strict=strict)
+
+    def update(self, scale_table=None, force: bool = False) -> bool:
+        """CompressionModel.update: build the entropy coders' CDF tables (required before compress())."""
+        from . import entropy_coding as EC_
+        if scale_table is None:
+            scale_table = EC_.get_scale_table()
+        updated = False
+        for m in self.modules():
+            if isinstance(m, EntropyBottleneck):
+                updated |= m.update(force=force)
+            elif isinstance(m, GaussianConditional):
+                updated |= m.update_scale_table(scale_table, force=force)
+        return updated
 
     def kernels(self, precision: str = "fp32"):
         """Whole-model HIP executor (used by the attack engine).  precision 'bf16': bf16-operand g_a / g_s
@@ -551,6 +650,17 @@ class FactorizedPrior(CompressionModel):
         x_hat = self.g_s(y_hat)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods}}
 
+    def compress(self, x):
+        """FactorizedPrior.compress: rANS bitstreams of round(g_a(x) - medians)."""
+        with torch.no_grad():
+            y = self.g_a(x)
+            return {"strings": [self.entropy_bottleneck.compress(y)], "shape": y.size()[-2:]}
+
+    def decompress(self, strings, shape):
+        with torch.no_grad():
+            y_hat = self.entropy_bottleneck.decompress(strings[0], shape)
+            return {"x_hat": self.g_s(y_hat).clamp_(0, 1)}
+
 
 class ScaleHyperprior(CompressionModel):
     model_kind = "hyper"
@@ -573,6 +683,44 @@ class ScaleHyperprior(CompressionModel):
         y_hat, y_likelihoods = self.gaussian_conditional(y, scales_hat)
         x_hat = self.g_s(y_hat)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+
+    def compress(self, x):
+        """ScaleHyperprior.compress: z -> EB bitstreams, scales = h_s(z_hat), y -> GC bitstreams.  One HIP pass
+        (g_a, h_a, symbols, h_s, symbols on nChw4c tensors), then rANS per image on host threads."""
+        from . import entropy_coding as EC_
+        eb, gc = self.entropy_bottleneck, self.gaussian_conditional
+        ztab, ytab = eb._coder_tables(), gc._coder_tables()
+        ck = self.kernels()
+        with torch.no_grad():
+            x4 = K.to_nc4(x.detach().contiguous())
+            y4, _ = ck.ga.forward(x4)
+            z4 = ck.ha.forward(y4)
+            B, _, zh, zw, _ = z4.shape
+            med = eb._get_medians().detach().reshape(-1).contiguous()
+            zs, zi = EC_.eb_symbols(z4, self.N, med)
+            z_hat4 = EC_.dequantize(zs, B, self.N, zh, zw, medians=med, device=x.device)
+            s4 = ck.hs.forward(z_hat4)
+            ys, yi = EC_.gc_symbols(y4, self.M, s4, None, gc.scale_table.to(x.device).contiguous(),
+                                    float(gc.scale_bound))
+            z_strings = EC_.encode_batch(zs, zi, ztab)
+            y_strings = EC_.encode_batch(ys, yi, ytab)
+        return {"strings": [y_strings, z_strings], "shape": torch.Size((zh, zw))}
+
+    def decompress(self, strings, shape):
+        from . import entropy_coding as EC_
+        eb, gc = self.entropy_bottleneck, self.gaussian_conditional
+        ytab = gc._coder_tables()
+        ck = self.kernels()
+        dev = self.entropy_bottleneck.quantiles.device
+        with torch.no_grad():
+            z_hat = eb.decompress(strings[1], shape)
+            s4 = ck.hs.forward(K.to_nc4(z_hat))
+            B, _, yh, yw, _ = s4.shape
+            _, yi = EC_.gc_symbols(s4, self.M, s4, None, gc.scale_table.to(dev).contiguous(), float(gc.scale_bound))
+            ys = EC_.decode_batch(strings[0], yi, ytab)
+            y_hat4 = EC_.dequantize(ys, B, self.M, yh, yw, device=dev)
+            xh4, _ = ck.gs.forward(ck._to_gs(y_hat4))
+            return {"x_hat": K.from_nc4(xh4, 3).clamp_(0, 1)}
 
 
 class Cheng2020Anchor(CompressionModel):

@@ -24,11 +24,15 @@
  *   EntropyBottleneck / GaussianConditional lik. ... anchors/model.py:86-108, anchors/balle.py:31-55 (CompressAI)
  *   bpp ............................................. attack_rd.py:419, self_ensemble.py:222
  *   MS-SSIM (pytorch_msssim / utils.torch_msssim) .. attack_rd.py:336,362; utils/torch_msssim.py:26-71
+ *   entropy coding (CompressAI compress/decompress, the _quantized_cdf / _offset / _cdf_length buffers
+ *     anchors/balle.py:57-72 restores) ............. ica_gc_symbols / ica_eb_symbols / ica_dequantize /
+ *                                                     ica_pmf_to_quantized_cdf / ica_rans_encode / ica_rans_decode
  */
 #ifndef ICA_HIP_H
 #define ICA_HIP_H
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -95,6 +99,27 @@ int ica_bitdepth_noise(const float* x, const float* u, float* y, long n, float s
 int ica_bitdepth_noise_bwd(const float* g, float* gx, long n, float scale, hipStream_t stream);
 int ica_add(const float* a, const float* b, float* y, long n, hipStream_t stream);
 int ica_ensemble_grad(const float* o, const float* out_s, float* g, long n, float invN, hipStream_t stream);
+/* Entropy coding (CompressAI EntropyBottleneck / GaussianConditional compress + decompress).
+ * Device: symbols / CDF indexes of nChw4c latents in NCHW order (int32), and dequantisation back to nChw4c.
+ *   ica_gc_symbols: idx = T-1 - #{j<T-1: max(scale, bound) <= table[j]}, sym = round(y - mean) (means4 may be NULL)
+ *   ica_eb_symbols: sym = round(z - medians[c]), idx = c
+ *   ica_dequantize: out = sym + (means4 ? means4 : medians ? medians[c] : 0)
+ * Host (plain pointers, no stream): 16-bit quantised CDFs and the 64-bit rANS coder (32-bit words, 4-bit bypass
+ * coding of values outside a table's range).  cdfs: n_cdfs rows of `stride` int32, row k valid for cdf_sizes[k]
+ * entries, offsets[k] = the value of slot 0.  ica_rans_encode returns the byte count (-7: cap too small, *needed
+ * holds the size; -5 bad table); ica_rans_decode returns 0 (-8 truncated / corrupt stream, -5 bad table). */
+int ica_gc_symbols(const float* y4, const float* scales4, const float* means4, const float* table, int T, float bound,
+                   int32_t* symbols, int32_t* indexes, int B, int C, int H, int W, hipStream_t stream);
+int ica_eb_symbols(const float* z4, const float* medians, int32_t* symbols, int32_t* indexes, int B, int C, int H,
+                   int W, hipStream_t stream);
+int ica_dequantize(const int32_t* symbols, const float* means4, const float* medians, float* out4, int B, int C, int H,
+                   int W, hipStream_t stream);
+int ica_pmf_to_quantized_cdf(const float* pmf, int n, int precision, int32_t* cdf_out);
+long ica_rans_encode(const int32_t* symbols, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
+                     const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, uint8_t* out, long cap,
+                     long* needed);
+int ica_rans_decode(const uint8_t* data, long nbytes, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
+                    const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols);
 /* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
  * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
  * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,
@@ -164,7 +189,7 @@ int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const f
                     float bc2s, float neg_step, int* branch, hipStream_t stream);
 /* Targeted / ROI attack (SURVEY §8f rank 1; README "attack with ROI", attack_cv.py:153-163 mask box,
  * attack_data.py:202-226 target / masked losses; semantics fixed in DESIGN.md).  Box [y0,y1) x [x0,x1) is the
- * target region; w_* are the per-element weights of the masked means (1/count, la_*/count).
+ * target region; w_* are the per-element weights of the masked means (1 / count, la_x / count).
  * prologue: im_in4 as ica_attack_prologue, part = box-weighted input distortion (loss_i after ica_reduce_rows).
  * loss: grad4 = d/dx_hat [w_out_tar * sum_tar (out_t - o)^2 + w_out_bkg * sum_bkg (out_s - o)^2], o = bound01(x_hat).
  * adam: ica_attack_adam with the box-weighted cheap-branch gradient. */

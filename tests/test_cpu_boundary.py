@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     txt = open(os.path.join(REPO, "include", "ica_hip.h")).read()
-    return sorted(set(re.findall(r"^(?:int|size_t)\s+(ica_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|long|size_t)\s+(ica_\w+)\s*\(", txt, re.M)))
 
 
 def test_library_exports_header_symbols():
