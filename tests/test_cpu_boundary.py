@@ -130,3 +130,15 @@ def test_aa_table_matches_torch_antialias_weights():
                 o[..., i] = acc
             t = np.moveaxis(o, -1, axis)
         assert float(np.abs(t - ref.numpy()).max()) < 2e-6
+
+
+def test_header_compiles_as_c_and_cpp():
+    """include/ica_hip.h is what a reference-side binding (ctypes / C / C++) reads: it must parse as C and C++."""
+    import shutil
+    import subprocess
+    hdr = os.path.join(REPO, "include", "ica_hip.h")
+    for cc, lang in (("gcc", "c"), ("g++", "c++")):
+        if shutil.which(cc) is None:
+            pytest.skip(f"{cc} not available")
+        r = subprocess.run([cc, "-fsyntax-only", "-x", lang, hdr], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
