@@ -605,6 +605,49 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_ke
     return v;
   };
   auto fill = [&](int ch) {
+    if constexpr (BF && CC == 16) {
+      // bf16 activations: the chunk's loads are issued in two batches of NB rows per thread (registers), the
+      // first one before the barrier that ends the previous chunk's reads: two memory latencies per fill
+      // instead of one per 256-entry row of the patch (the whole chunk at once spilled)
+      static_assert(!BF || FX == 0, "bf16 conv_down fill: plain view only");
+      constexpr int NF = (NE * PLANE + 255) / 256, NB = (NF + 1) / 2;
+      // buffer loads with 32-bit lane offsets into this image (no 64-bit address registers); padding and
+      // entries past the patch read out of the descriptor's range, which returns zeros
+      const unsigned xplane = (unsigned)p.Hin * p.Win;
+      const __amdgpu_buffer_rsrc_t xr =
+          uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 8, Cin4 * xplane * 8u);
+      auto batch = [&](int i0, u32x2 (&va)[NB], u32x2 (&vb)[NB]) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int e = threadIdx.x + 256 * (i0 + i);
+          const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+          const int iy = iy0 + pr, ix = ix0 + pc;
+          const int c4 = ch * NQ + 2 * q;
+          const bool ok = i0 + i < NF && e < NE * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 &&
+                          ix < p.Win;
+          const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 8u;
+          va[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+          vb[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo + xplane * 8u : 0xFFFFFFF0u,
+                                                                                 0, 0));
+        }
+      };
+      auto put = [&](int i0, const u32x2 (&va)[NB], const u32x2 (&vb)[NB]) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int e = threadIdx.x + 256 * (i0 + i);
+          if (i0 + i < NF && e < NE * PLANE)
+            patch[e] = __builtin_bit_cast(f32x4, (u32x4_t){va[i][0], va[i][1], vb[i][0], vb[i][1]});
+        }
+      };
+      u32x2 va[NB], vb[NB];
+      batch(0, va, vb);
+      __syncthreads();
+      put(0, va, vb);
+      batch(NB, va, vb);
+      put(NB, va, vb);
+      __syncthreads();
+      return;
+    }
     __syncthreads();
     for (int e = threadIdx.x; e < NE * PLANE; e += 256) {
       const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
@@ -819,6 +862,9 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
         for (int it = 0; it < IT; ++it) a[it] = ICA_WLOAD_BF(w, it, u);
       };
       auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int u) {
+        // one scheduling region per step: the ring's loads stay 3 steps ahead of their MFMAs (without it the
+        // scheduler sank one set next to its use, a full L2-latency wait per 4 steps)
+        __builtin_amdgcn_sched_barrier(0);
         ldw(nxt, u + 3);
         const int po = poff(u);
         bf16x8 b[PT];
@@ -910,7 +956,11 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int jt = wave & 1, nch = p.Cin / 16;
   // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
+#ifdef ICA_ABLATE_SAMECLASS
+  if (true) {  // timing-only: every wave runs the first class pair (4 waves share weights; wrong results)
+#else
   if (wave < 2) {
+#endif
     conv_up_class<KS, 0, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
     __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
     conv_up_class<KS, 1, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
