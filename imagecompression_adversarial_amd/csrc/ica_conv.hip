@@ -984,9 +984,10 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
 // --------------------------------------------------------------------------
 constexpr int T3_TH = 8, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 340
 constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                            // 11
+constexpr int T3_NCH_BF = 8;  // bf16 up-front-load path: Cin = 128
 
 template <bool BF>
-__global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, 1) void conv_up3_kernel(ConvParams p) {
   __shared__ float zs[T3_ROWS * T3_NPX];
   const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
   int bid = blockIdx.x;
@@ -999,6 +1000,66 @@ __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int Cin4 = p.Cin >> 2, nch = p.Cin / 16;
   const size_t plane = (size_t)p.Hin * p.Win;
+  if constexpr (BF) {
+    if (nch == T3_NCH_BF) {
+      // bf16, Cin = 128 (the N = 128 models): the Z GEMM is latency-bound at one block per CU (the 102 KB Z
+      // tile), so every load of the block is issued up front: all 24 weight fragments (once per block, L2) and
+      // the 8 chunks of each of this wave's (<= 3) pixel tiles (HBM, buffer loads with 32-bit offsets;
+      // out-of-image pixels read past the descriptor and get zeros), then the tiles' MFMAs and Z stores.
+      constexpr int MJ = (T3_JT + 3) / 4;
+      const bf16x8* wl = reinterpret_cast<const bf16x8*>(p.wp) + lane;
+      bf16x8 wa[T3_NCH_BF][3];
+#pragma unroll
+      for (int ch = 0; ch < T3_NCH_BF; ++ch)
+#pragma unroll
+        for (int it = 0; it < 3; ++it) wa[ch][it] = wl[((size_t)it * T3_NCH_BF + ch) * 64];
+      const unsigned img_bytes = (unsigned)(Cin4 * plane * 8);
+      const __amdgpu_buffer_rsrc_t xr =
+          uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * img_bytes, img_bytes);
+      u32x2 xa[MJ][T3_NCH_BF][2];
+#pragma unroll
+      for (int k = 0; k < MJ; ++k) {
+        const int q = (wave + 4 * k) * 32 + j;
+        const int hr = q / T3_HC, hc = q - hr * T3_HC;
+        const int iy = a0 - 1 + hr, ix = b0 - 1 + hc;
+        const bool ok = wave + 4 * k < T3_JT && q < T3_NPX && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+        const unsigned po = (unsigned)(iy * p.Win + ix) * 8u;
+#pragma unroll
+        for (int ch = 0; ch < T3_NCH_BF; ++ch)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const unsigned vo = ok ? po + (unsigned)((4 * ch + 2 * h + e) * plane) * 8u : 0xFFFFFFF0u;
+            xa[k][ch][e] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, vo, 0, 0));
+          }
+      }
+#pragma unroll
+      for (int k = 0; k < MJ; ++k) {
+        const int jt = wave + 4 * k;
+        if (jt >= T3_JT) break;
+        const int q = jt * 32 + j;
+        f32x16 acc[3];
+#pragma unroll
+        for (int it = 0; it < 3; ++it) acc[it] = f32x16{0};
+#pragma unroll
+        for (int ch = 0; ch < T3_NCH_BF; ++ch) {
+          const bf16x8 b = __builtin_bit_cast(bf16x8, (u32x4_t){xa[k][ch][0][0], xa[k][ch][0][1], xa[k][ch][1][0],
+                                                                 xa[k][ch][1][1]});
+#pragma unroll
+          for (int it = 0; it < 3; ++it) acc[it] = mfma32bf(wa[ch][it], b, acc[it]);
+        }
+        if (q < T3_NPX) {
+#pragma unroll
+          for (int it = 0; it < 3; ++it)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = it * 32 + acc_row(r, h);
+              if (row < T3_ROWS) zs[row * T3_NPX + q] = acc[it][r];
+            }
+        }
+      }
+      goto gather;
+    }
+  }
   for (int jt = wave; jt < T3_JT; jt += 4) {
     const int q = jt * 32 + j;
     const int hr = q / T3_HC, hc = q - hr * T3_HC;
@@ -1090,6 +1151,7 @@ __global__ __launch_bounds__(256) void conv_up3_kernel(ConvParams p) {
         }
     }
   }
+gather:
   __syncthreads();
   // gather: thread -> input pixel (a, b) of the owned tile, 4 classes x 3 channels
   const int al = threadIdx.x / T3_TW, bl = threadIdx.x % T3_TW;
