@@ -207,9 +207,16 @@ def main():
     dom_flops = flops_of[dom]
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     peak = BF16_MFMA_PEAK_TFLOPS if (args.precision == "bf16" and dom in _bf16_tags(kern)) else FP32_MFMA_PEAK_TFLOPS
+    # HBM bytes per launch of the dominant kernel from the committed PMC passes of the same shapes
+    # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)
     traffic = None
-    tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf) and args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32):
+    tfile = None
+    if args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32):
+        tfile = "pmc_traffic.json"
+    elif args.precision == "bf16" and (H, W, B) == (2048, 2048, 8):
+        tfile = "pmc_traffic_c5.json"
+    tf = os.path.join(REPO, "profiles", tfile) if tfile else None
+    if tf and os.path.exists(tf):
         try:
             traffic = json.load(open(tf)).get(dom)
         except Exception:

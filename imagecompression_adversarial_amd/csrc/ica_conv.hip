@@ -853,20 +853,42 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
   };
   if constexpr (NY * NX > 0) {
     if constexpr (BF) {
-      // bf16: 4-set weight-fragment ring, prefetch distance 3 (see conv_down_kernel)
+      // bf16: 4-set weight-fragment ring, prefetch distance 3 (see conv_down_kernel).  The (tap, chunk) walk
+      // u -> (ti, ch) runs on scalar counters (no runtime division by nch: at one 32-cycle MFMA per tile that
+      // scalar arithmetic was ~10 SALU per MFMA and kept the MFMA pipe a quarter busy); LDS address = a
+      // per-lane base + a wave-uniform (tap, chunk) offset.
+      constexpr int NT = NY * NX;
       const bf16x8* wb = reinterpret_cast<const bf16x8*>(p.wp) + (size_t)cb * KS * KS * nch * IT * 64 + lane;
-      bf16x8 fr[4][IT];
-      auto ldw = [&](bf16x8 (&a)[IT], int u) {
-        const bf16x8* w = wb + woff(min(u, total - 1)) * IT * 64;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) a[it] = ICA_WLOAD_BF(w, it, u);
+      const int lane_off = h * UP_PLANE + (a_rel + 1) * UP_PC + (b_rel + 1);
+      auto tap_lds = [&](int ti) -> int {
+        const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+        return ((PY + PAD - ky) / 2) * UP_PC + (PX + PAD - kx) / 2;
       };
-      auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int u) {
+      auto tap_w = [&](int ti) -> int {
+        const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+        return ky * KS + kx;
+      };
+      int ti_c = 0, ch_c = 0, ti_w = 0, ch_w = 0;
+      auto adv = [&](int& ti, int& ch) {
+        ch = ch + 1 == nch ? 0 : ch + 1;
+        ti = ch == 0 ? ti + 1 : ti;
+      };
+      bf16x8 fr[4][IT];
+      auto ldw = [&](bf16x8 (&a)[IT]) {   // the fragment set of step (ti_w, ch_w), clamped to the last step
+        const bool past = ti_w >= NT;
+        const int wo = tap_w(past ? NT - 1 : ti_w) * nch + (past ? nch - 1 : ch_w);
+        const bf16x8* w = wb + (size_t)wo * IT * 64;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) a[it] = ICA_WLOAD_BF(w, it, wo);
+        adv(ti_w, ch_w);
+      };
+      auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT]) {
         // one scheduling region per step: the ring's loads stay 3 steps ahead of their MFMAs (without it the
         // scheduler sank one set next to its use, a full L2-latency wait per 4 steps)
         __builtin_amdgcn_sched_barrier(0);
-        ldw(nxt, u + 3);
-        const int po = poff(u);
+        ldw(nxt);
+        const int po = lane_off + 2 * ch_c * UP_PLANE + tap_lds(ti_c);
+        adv(ti_c, ch_c);
         bf16x8 b[PT];
 #pragma unroll
         for (int t = 0; t < PT; ++t) b[t] = f4_as_bf8(patch[po + t * 2 * UP_PC]);   // tile t: 2 rows down
@@ -875,20 +897,20 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
 #pragma unroll
           for (int it = 0; it < IT; ++it) acc[t][it] = mfma32bf(cur[it], b[t], acc[t][it]);
       };
-      ldw(fr[0], 0);
-      ldw(fr[1], 1);
-      ldw(fr[2], 2);
+      ldw(fr[0]);
+      ldw(fr[1]);
+      ldw(fr[2]);
       int u = 0;
 #pragma unroll 1
       for (; u + 4 <= total; u += 4) {
-        step(fr[0], fr[3], u);
-        step(fr[1], fr[0], u + 1);
-        step(fr[2], fr[1], u + 2);
-        step(fr[3], fr[2], u + 3);
+        step(fr[0], fr[3]);
+        step(fr[1], fr[0]);
+        step(fr[2], fr[1]);
+        step(fr[3], fr[2]);
       }
-      if (u < total) step(fr[0], fr[3], u);
-      if (u + 1 < total) step(fr[1], fr[0], u + 1);
-      if (u + 2 < total) step(fr[2], fr[1], u + 2);
+      if (u < total) step(fr[0], fr[3]);
+      if (u + 1 < total) step(fr[1], fr[0]);
+      if (u + 2 < total) step(fr[2], fr[1]);
     } else {
       // weight fragments prefetched one step ahead into the other of two register sets (ping-pong)
       const float* wl = p.wp + (size_t)cb * KS * KS * nch * WSTEP + (size_t)lane * 8;
@@ -935,22 +957,37 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   const int a0 = ty * UP_TH, b0 = tx * UP_TW;
   const int Cin4 = p.Cin >> 2;  // Cin % 16 == 0 enforced by host
   const int total = (BF ? Cin4 / 2 : Cin4) * UP_PLANE;
-  for (int e = threadIdx.x; e < total; e += 256) {
-    const int q = e / UP_PLANE, rem = e - q * UP_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
-    const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
-    const bool ok = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const size_t xo = (((size_t)n * Cin4 + (BF ? 2 * q : q)) * p.Hin + iy) * p.Win + ix;  // quad index
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (BF) {  // bf16 activations: two 8-B channel quads per 16-B LDS entry
-      if (ok) {
-        const u32x2* xb = reinterpret_cast<const u32x2*>(p.x) + xo;
-        const u32x2 a = xb[0], b = xb[(size_t)p.Hin * p.Win];
-        v = __builtin_bit_cast(f32x4, (u32x4_t){a[0], a[1], b[0], b[1]});
+  // The patch fill: batches of UP_FB entries per thread whose loads are all issued before their LDS writes
+  // (buffer loads with 32-bit offsets into this image; padding pixels read past the descriptor and get
+  // zeros), so the fill costs one memory latency per batch instead of one per entry.
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const unsigned qbytes = BF ? 8u : 16u;
+  const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(
+      reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * qbytes, Cin4 * xplane * qbytes);
+  constexpr int UP_FB = 8;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * UP_FB) {
+    u32x4_t v[UP_FB];
+#pragma unroll
+    for (int i = 0; i < UP_FB; ++i) {
+      const int e = e0 + 256 * i;
+      const int q = e / UP_PLANE, rem = e - q * UP_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
+      const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+      const bool ok = e < total && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)(BF ? 2 * q : q) * xplane + (unsigned)iy * p.Win + ix) * qbytes;
+      if constexpr (BF) {  // bf16 activations: two 8-B channel quads per 16-B LDS entry
+        const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+        const u32x2 hi = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo + xplane * 8u : 0xFFFFFFF0u, 0, 0));
+        v[i] = (u32x4_t){lo[0], lo[1], hi[0], hi[1]};
+      } else {
+        v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
       }
-    } else {
-      if (ok) v = ld4(p.x + xo * 4);
     }
-    patch[e] = v;
+#pragma unroll
+    for (int i = 0; i < UP_FB; ++i) {
+      const int e = e0 + 256 * i;
+      if (e < total) patch[e] = __builtin_bit_cast(f32x4, v[i]);
+    }
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

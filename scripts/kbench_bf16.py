@@ -1,12 +1,18 @@
 """Per-kernel timing of the bf16 conv kernels at BASELINE config-5 shapes (hyper q3, 8 x 2048x2048):
 level-1 (1024^2) <-> level-2 (512^2) layers and the RGB ends.  Median of 7 launches (HIP events, launch
 stream), printed with algorithmic TFLOP/s and the HBM bytes of the activation tensors they move.
-    python scripts/kbench_bf16.py [lib path]     (lib path: e.g. an ICA_ABLATE_* build)"""
+    python scripts/kbench_bf16.py [lib path] [--only name-substring]   (lib path: e.g. an ICA_ABLATE_* build)"""
 import os
 import sys
 
-if len(sys.argv) > 1:
-    os.environ["ICA_HIP_LIB"] = os.path.abspath(sys.argv[1])
+ONLY = None
+args = sys.argv[1:]
+if "--only" in args:
+    i = args.index("--only")
+    ONLY = args[i + 1]
+    del args[i:i + 2]
+if args:
+    os.environ["ICA_HIP_LIB"] = os.path.abspath(args[0])
 sys.path.insert(0, ".")
 import torch  # noqa: E402
 
@@ -51,6 +57,8 @@ cases = {
     "up3        (g_s.6.fwd)": (lambda: K.conv_up(x1, N, w6.fwd, w6.bias, 3, prec=1), FL0),
 }
 for name, (fn, fl) in cases.items():
+    if ONLY and ONLY not in name:
+        continue
     fn()
     torch.cuda.synchronize()
     ts = []

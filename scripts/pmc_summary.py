@@ -38,8 +38,9 @@ for _, (k, g), m, t in rows[:16]:
         out.append(f"fetchKB(x2)={2 * m['FETCH_SIZE']:.0f}")
     if "WRITE_SIZE" in m:
         out.append(f"writeKB={m['WRITE_SIZE']:.0f}")
-    for c in ("SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_LDS_BANK_CONFLICT",
-              "SQ_WAIT_INST_LDS"):
+    for c in ("SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+              "SQ_INSTS_SALU", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "TCP_TOTAL_CACHE_ACCESSES_sum",
+              "TCP_TCC_READ_REQ_sum", "TCC_HIT_sum", "TCC_MISS_sum"):
         if c in m:
             out.append(f"{c[8:]}={m[c]:.3g}")
     print(" | ".join(out))

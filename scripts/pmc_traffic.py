@@ -28,12 +28,14 @@ def tw(Wout):
 
 def down(cc, epi, Hout, Wout, Cout, it):
     t = tw(Wout)
-    grid = -(-Wout // t) * -(-Hout // TH[t]) * B * 256 * -(-Cout // (it * 32))
+    th = (256 if (PREC == "bf16" and cc == 16) else 128) // t   # bf16 16-channel chunks: 2 pixel tiles per wave
+    grid = -(-Wout // t) * -(-Hout // th) * B * 256 * -(-Cout // (it * 32))
     return f"void conv_down_kernel<5, 2, {it}, {cc}, {t}, {epi}, 0, {BF}>", grid
 
 
 def up(epi, Hin, Win, Cout, it):
-    return f"void conv_up_kernel<5, {it}, {epi}, 0, {BF}>", -(-Win // 16) * -(-Hin // 4) * B * 256 * -(-Cout // (it * 32))
+    th = 8 if PREC == "bf16" else 4   # bf16: two 32-pixel tiles per class per wave
+    return f"void conv_up_kernel<5, {it}, {epi}, 0, {BF}>", -(-Win // 16) * -(-Hin // th) * B * 256 * -(-Cout // (it * 32))
 
 
 def up3(Hin, Win):
