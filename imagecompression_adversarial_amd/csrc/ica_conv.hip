@@ -891,7 +891,12 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
         adv(ti_c, ch_c);
         bf16x8 b[PT];
 #pragma unroll
+#ifdef ICA_ABLATE_BLDS
+        for (int t = 0; t < PT; ++t) b[t] = cur[t];   // timing-only: no LDS operand reads (wrong results)
+        (void)po;
+#else
         for (int t = 0; t < PT; ++t) b[t] = f4_as_bf8(patch[po + t * 2 * UP_PC]);   // tile t: 2 rows down
+#endif
 #pragma unroll
         for (int t = 0; t < PT; ++t)
 #pragma unroll
