@@ -648,6 +648,46 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_ke
       __syncthreads();
       return;
     }
+    if constexpr (!BF && CC == 16 && FX == 0) {
+      // fp32 plain view: batches of FB 16-B buffer loads (32-bit offsets, out-of-image reads return zeros)
+      // issued before their LDS writes, the first batch ahead of the barrier that ends the previous chunk's
+      // reads.  FB is kept small: these kernels run 3 waves/SIMD at <= 168 VGPRs.
+      constexpr int NF = (NE * PLANE + 255) / 256, FB = 3;
+      const unsigned xplane = (unsigned)p.Hin * p.Win;
+      const __amdgpu_buffer_rsrc_t xr =
+          uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+      auto batch = [&](int i0, u32x4_t (&v)[FB]) {
+#pragma unroll
+        for (int i = 0; i < FB; ++i) {
+          const int e = threadIdx.x + 256 * (i0 + i);
+          const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+          const int iy = iy0 + pr, ix = ix0 + pc;
+          const int c4 = ch * NQ + q;
+          const bool ok = i0 + i < NF && e < NE * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 &&
+                          ix < p.Win;
+          const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+          v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+        }
+      };
+      auto put = [&](int i0, const u32x4_t (&v)[FB]) {
+#pragma unroll
+        for (int i = 0; i < FB; ++i) {
+          const int e = threadIdx.x + 256 * (i0 + i);
+          if (i0 + i < NF && e < NE * PLANE) patch[e] = __builtin_bit_cast(f32x4, v[i]);
+        }
+      };
+      u32x4_t v[FB];
+      batch(0, v);
+      __syncthreads();
+      put(0, v);
+#pragma unroll
+      for (int i0 = FB; i0 < NF; i0 += FB) {
+        batch(i0, v);
+        put(i0, v);
+      }
+      __syncthreads();
+      return;
+    }
     __syncthreads();
     for (int e = threadIdx.x; e < NE * PLANE; e += 256) {
       const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
