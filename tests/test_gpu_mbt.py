@@ -148,3 +148,27 @@ def test_mbt_cli_runs(capsys):
     txt = capsys.readouterr().out
     assert "AVG: context-mse-5" in txt
     assert out["bpp_ori"] > 0
+
+
+def test_mbt_image_coder_and_probe(mbt3):
+    """anchors.balle.Image_coder("context") tuple and anchors.model.probe(means_hat) against the oracle."""
+    from imagecompression_adversarial_amd.anchors import balle
+    from imagecompression_adversarial_amd.anchors import model as am
+    P, _ = mbt3
+    ic = balle.Image_coder("context", 3, "mse", pretrained=False)
+    sd = ic.net.state_dict()
+    sd.update({k: v.reshape(sd[k].shape) for k, v in P.items()})
+    ic.net.load_state_dict(sd)
+    ic = ic.to(DEV)
+    x = rnd((1, 3, 128, 128), 51, 0.0, 1.0)
+    with torch.no_grad():
+        x_hat, y, z_hat, y_lik, z_lik = ic(x.to(DEV), False, True, False)
+        means = am.probe(x.to(DEV), ic.net, "means_hat", "context")
+    ref = oc.forward(P, x, "context")
+    assert rel_err(x_hat.cpu(), ref["x_hat"]) < 2e-4
+    assert rel_err(y_lik.cpu(), ref["likelihoods"]["y"]) < 1e-3
+    assert rel_err(z_lik.cpu(), ref["likelihoods"]["z"]) < 1e-3
+    yr = oc.g_a(P, x)
+    zh, _ = oc.entropy_bottleneck(P, oc.mbt_h_a(P, yr))
+    gp = oc.entropy_parameters(P, torch.cat((oc.mbt_h_s(P, zh), oc.context_prediction(P, torch.round(yr))), 1))
+    assert rel_err(means.cpu(), gp.chunk(2, 1)[1]) < 2e-4
