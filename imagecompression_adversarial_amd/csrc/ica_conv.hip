@@ -862,8 +862,8 @@ constexpr int up_plane() { return (up_th<BF>() + 2) * UP_PC; }
 // cheng2020's conv3x3 s2 and conv1x1 s2 skips).  Output y = 2a + PY uses taps
 // ky = ky0 + 2i, ky0 = (PY + PAD) & 1, at input row iy = a + (PY + PAD - ky) / 2 in [a-1, a+1].
 template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF>
-ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
-                           int nch) {
+ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch,
+                         f32x16 (&acc)[up_pt<BF>()][IT]) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   constexpr int PT = up_pt<BF>(), UP_PLANE = up_plane<BF>();
   // pixel tile t of this wave: input rows (jt*PT + t)*2 + (j>>4) of the block tile, columns j&15
@@ -872,7 +872,6 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
   constexpr int PAD = KS / 2;
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2;  // taps per axis
-  f32x16 acc[PT][IT];
 #pragma unroll
   for (int t = 0; t < PT; ++t)
 #pragma unroll
@@ -980,10 +979,53 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
       if (u < total) step(fa, fb, u);
     }
   }
+}
+
+// the epilogue of class (PY, PX) for the pixel tiles of row group jt
+template <int PY, int PX, int IT, int EPI, int FX, bool BF>
+ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], int n, int a0, int b0, int jt,
+                           int cb) {
+  constexpr int PT = up_pt<BF>();
+  const int j = threadIdx.x & 31;
+  const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
     conv_epilogue<IT, EPI, FX, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  }
+}
+
+template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF>
+ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
+                           int nch) {
+  f32x16 acc[up_pt<BF>()][IT];
+  conv_up_acc<KS, PY, PX, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc);
+  conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb);
+}
+
+// fp32 forward epilogues (stores only): both classes' main loops first, then both epilogues.  The first class's
+// output stores, issued before the second class's main loop, made that loop's weight-prefetch waits (vmcnt
+// counts stores too) wait for the stores to drain.  The 64 extra accumulator registers fit the 2 waves/SIMD
+// these kernels run at.
+template <int KS, int IT, int EPI, int FX, bool BF>
+constexpr bool up_defer() {
+  return !BF && IT <= 4 && FX == 0 &&
+         (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_LRELU || EPI == EPI_IGDN || EPI == EPI_GDN);
+}
+template <int KS, int PY0, int PX0, int PY1, int PX1, int IT, int EPI, int FX, bool BF>
+ICA_DEV void conv_up_pair(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb, int nch) {
+  if constexpr (up_defer<KS, IT, EPI, FX, BF>()) {
+    f32x16 acc0[up_pt<BF>()][IT], acc1[up_pt<BF>()][IT];
+    conv_up_acc<KS, PY0, PX0, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc0);
+    __builtin_amdgcn_sched_barrier(0);
+    conv_up_acc<KS, PY1, PX1, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc1);
+    __builtin_amdgcn_sched_barrier(0);
+    conv_up_store<PY0, PX0, IT, EPI, FX, BF>(p, acc0, n, a0, b0, jt, cb);
+    conv_up_store<PY1, PX1, IT, EPI, FX, BF>(p, acc1, n, a0, b0, jt, cb);
+  } else {
+    conv_up_class<KS, PY0, PX0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
+    conv_up_class<KS, PY1, PX1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   }
 }
 
@@ -1043,13 +1085,9 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
 #else
   if (wave < 2) {
 #endif
-    conv_up_class<KS, 0, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
-    __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
-    conv_up_class<KS, 1, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_pair<KS, 0, 0, 1, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   } else {
-    conv_up_class<KS, 0, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
-    __builtin_amdgcn_sched_barrier(0);
-    conv_up_class<KS, 1, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_pair<KS, 0, 1, 1, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   }
 }
 
