@@ -648,8 +648,8 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_ke
       __syncthreads();
       return;
     }
-    if constexpr (!BF && CC == 16 && FX == 0) {
-      // fp32 plain view: batches of FB 16-B buffer loads (32-bit offsets, out-of-image reads return zeros)
+    if constexpr (!BF && CC == 16 && (FX & (FX_MASK | FX_UNSHUF)) == 0) {
+      // fp32 plain view (any epilogue extras): batches of FB 16-B buffer loads (32-bit offsets, out-of-image reads return zeros)
       // issued before their LDS writes, the first batch ahead of the barrier that ends the previous chunk's
       // reads.  FB is kept small: these kernels run 3 waves/SIMD at <= 168 VGPRs.
       constexpr int NF = (NE * PLANE + 255) / 256, FB = 3;
