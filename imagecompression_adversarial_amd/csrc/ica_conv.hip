@@ -547,12 +547,12 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_ke
   __shared__ f32x4 patch[NE * PLANE];
 
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
-  int bid = blockIdx.x;
+  int bid, cb;
+  xcd_block<BF>(bid, cb);
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int n = bid / tiles_y;
-  const int cb = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
@@ -1035,12 +1035,12 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   constexpr int UP_TH = up_th<BF>(), UP_PLANE = up_plane<BF>();
   const int Hh = p.Hin, Wh = p.Win;
   const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UP_TH - 1) / UP_TH;
-  int bid = blockIdx.x;
+  int bid, cb;
+  xcd_block<BF>(bid, cb);
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int n = bid / tiles_y;
-  const int cb = blockIdx.y;
   const int a0 = ty * UP_TH, b0 = tx * UP_TW;
   const int Cin4 = p.Cin >> 2;  // Cin % 16 == 0 enforced by host
   const int total = (BF ? Cin4 / 2 : Cin4) * UP_PLANE;
@@ -1110,7 +1110,9 @@ template <bool BF>
 __global__ __launch_bounds__(256, 1) void conv_up3_kernel(ConvParams p) {
   __shared__ float zs[T3_ROWS * T3_NPX];
   const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
-  int bid = blockIdx.x;
+  int bid, by;
+  xcd_block<BF>(bid, by);
+  (void)by;  // one channel block
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
