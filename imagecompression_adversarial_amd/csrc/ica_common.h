@@ -105,9 +105,9 @@ ICA_DEV constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 
 // XCD-aware block order (a speed choice only; used by the bf16 conv kernels, +2-3 % on config 5, while the
 // MFMA-bound fp32 kernels measured neutral to -1 % and keep the plain order).  Workgroups are dealt
 // round-robin over the 8 XCDs by linear id, so neighbouring conv tiles (which share patch halo rows) land
-// on different private L2s.  Remap the
-// linear id so each XCD gets one contiguous run of (tile, channel-block) ids: q = total/8, r = total%8,
-// XCD x = lin%8 takes ids [x*q + min(x,r), ... + q + (x<r)) in dispatch order (a bijection for any total).
+// on different private L2s.  Remap the linear id so each XCD gets one contiguous run of (tile,
+// channel-block) ids: q = total/8, r = total%8, XCD x = lin%8 takes ids [x*q + min(x,r), ... + q + (x<r))
+// in dispatch order (a bijection for any total).
 template <bool REMAP>
 ICA_DEV void xcd_block(int& bx, int& by) {
   const unsigned nx = gridDim.x, total = nx * gridDim.y;

@@ -532,8 +532,12 @@ constexpr int down_pt() { return (BF && CC == 16) ? 2 : 1; }
 template <int KS, int IT>
 constexpr int conv_min_blocks() { return (KS == 5 && IT == 6) ? 1 : 2; }
 
+// the bf16 RGB-input GDN forward (g_a's first layer, store-bound) fits 128 VGPRs: 4 waves/SIMD
+template <int KS, int IT, int CC, int EPI, bool BF>
+constexpr int conv_down_waves() { return (BF && CC == 4 && EPI == EPI_GDN) ? 4 : conv_min_blocks<KS, IT>(); }
+
 template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
-__global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
   constexpr int PT = down_pt<CC, BF>();
   constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
@@ -684,6 +688,41 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_down_ke
       for (int i0 = FB; i0 < NF; i0 += FB) {
         batch(i0, v);
         put(i0, v);
+      }
+      __syncthreads();
+      return;
+    }
+    if constexpr (CC == 4 && FX == 0) {
+      // RGB input (one 4-channel plane, one fill per block): every entry of this thread (NF = 3 for the
+      // k5 s2 tiles) is loaded up front with 16-B buffer loads (32-bit offsets; padding reads past the
+      // descriptor and returns zeros), one memory latency instead of NF dependent rounds.
+      constexpr int NF = (NE * PLANE + 255) / 256;
+      const unsigned xplane = (unsigned)p.Hin * p.Win;
+      const __amdgpu_buffer_rsrc_t xr =
+          uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+      u32x4_t v[NF];
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+        const int iy = iy0 + pr, ix = ix0 + pc;
+        const int c4 = ch * NQ + q;
+        const bool ok = e < NE * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+        const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+        v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        if (e < NE * PLANE) {
+          f32x4 f = __builtin_bit_cast(f32x4, v[i]);
+          const int c4 = ch * NQ + e / PLANE;
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2)
+            if (c4 * 4 + e2 >= p.Cin) f[e2] = 0.f;
+          patch[e] = f;
+        }
       }
       __syncthreads();
       return;
