@@ -1136,17 +1136,23 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
 // output channels to a 32-row MFMA tile (10.7x waste).  Instead:
 //   Z[(co,ky,kx)][pixel] = sum_ci W[ci][co][ky][kx] * x[ci][pixel]   (75 x Cin dense GEMM)
 //   out[co][2a+py][2b+px] = sum_{ky=py, kx=px (mod 2)} Z[(co,ky,kx)][a+dy, b+dx]
-// The block owns an 8x32 input-pixel tile; Z is computed for its 10x34 halo
-// tile into LDS (75 x 340 floats), then each thread gathers the 12 outputs of
-// one input pixel.  Weight fragments packed [it(3)][chunk][lane][8] with row
+// The block owns a 6x32 input-pixel tile; Z is computed for its 8x34 halo
+// tile into LDS (75 x 272 floats = 81600 B, so two blocks share a CU's 160 KB and one block's Z GEMM
+// overlaps the other's gather and loads; the 8x32 tile's 102 KB Z allowed one block per CU, whose
+// phases then ran back to back), then each thread of the first 6 rows gathers the 12 outputs of one
+// input pixel.  Weight fragments packed [it(3)][chunk][lane][8] with row
 // o = it*32 + (lane&31) = co*25 + ky*5 + kx.
 // --------------------------------------------------------------------------
-constexpr int T3_TH = 8, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 340
-constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                            // 11
+#ifndef ICA_T3_TH
+#define ICA_T3_TH 6
+#endif
+constexpr int T3_TH = ICA_T3_TH, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 272
+constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                                // 9
 constexpr int T3_NCH_BF = 8;  // bf16 up-front-load path: Cin = 128
+constexpr int T3_BLOCKS = (2 * T3_ROWS * T3_NPX * 4 <= 160 * 1024) ? 2 : 1;
 
 template <bool BF>
-__global__ __launch_bounds__(256, 1) void conv_up3_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) {
   __shared__ float zs[T3_ROWS * T3_NPX];
   const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
   int bid, by;
@@ -1317,7 +1323,7 @@ gather:
   // gather: thread -> input pixel (a, b) of the owned tile, 4 classes x 3 channels
   const int al = threadIdx.x / T3_TW, bl = threadIdx.x % T3_TW;
   const int a = a0 + al, b = b0 + bl;
-  if (a >= p.Hin || b >= p.Win) return;
+  if (al >= T3_TH || a >= p.Hin || b >= p.Win) return;
   const float bias0 = p.bias ? p.bias[0] : 0.f, bias1 = p.bias ? p.bias[1] : 0.f, bias2 = p.bias ? p.bias[2] : 0.f;
 #pragma unroll
   for (int py = 0; py < 2; ++py) {
