@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   const int Hh = p.Hin, Wh = p.Win;
   const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UP_TH - 1) / UP_TH;
   int bid, cb;
-  xcd_block<BF>(bid, cb);
+  xcd_block<true>(bid, cb);  // both precisions: the fp32 GDN-bwd layer's HBM reads drop with the halo rows L2-shared
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
