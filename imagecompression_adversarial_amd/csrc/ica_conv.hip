@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
 
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
   int bid, cb;
-  xcd_block<BF || CC == 4>(bid, cb);
+  xcd_block<BF>(bid, cb);
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
@@ -1156,7 +1156,7 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
   __shared__ float zs[T3_ROWS * T3_NPX];
   const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
   int bid, by;
-  xcd_block<true>(bid, by);
+  xcd_block<BF>(bid, by);
   (void)by;  // one channel block
   const int tx = bid % tiles_x;
   bid /= tiles_x;
