@@ -144,12 +144,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ICA_BENCH_DIST_BACKEND=gloo rehearses the N>1 path with every rank on the box's GPUs modulo their
+    # count (one-GPU boxes); the driver's multi-GPU runs use the default, RCCL with one GPU per rank
+    backend = os.environ.get("ICA_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from imagecompression_adversarial_amd import codec as models
     from imagecompression_adversarial_amd import hip_ops as K
