@@ -832,6 +832,39 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
     if (g < total) step(fr[0], fr[3], g);
     if (g + 1 < total) step(fr[1], fr[0], g + 1);
     if (g + 2 < total) step(fr[2], fr[1], g + 2);
+  } else if constexpr (CC == 4) {
+    // fp32 RGB input, packed K (pack_conv_kernel, CC = 4): k-step m = 2g + s2 of step g takes the (tap,
+    // channel) pair f = 2m + h from lane half h, f running over tap*Cin + channel.  With Cin = 3 that is
+    // ceil(75/4) = 19 steps of 2 MFMA k-steps instead of 25 taps x (3 channels + 1 zero pad).
+    fill(0);
+    const int Cp = p.Cin;
+    const int NS = (KK * Cp + 3) / 4;
+    const float* wptr = p.wp + (size_t)cb * KK * WSTEP + (size_t)lane * KH;
+    const float* pf = reinterpret_cast<const float*>(patch);
+    auto bval = [&](int f) -> float {
+      int tap = f / Cp;
+      const int c = f - tap * Cp;
+      tap = min(tap, KK - 1);  // past the list: zero weight, read any finite patch value
+      const int ky = tap / KS, kx = tap - ky * KS;
+      return pf[4 * (lbase + ky * PC + kx) + c];
+    };
+    auto step = [&](float (&cur)[IT][KH], float (&nxt)[IT][KH], int g) {
+      load_frag<IT, KH>(nxt, wptr + (size_t)min(g + 1, NS - 1) * WSTEP);  // unconditional: no phi copies
+      const float b[2] = {bval(4 * g + h), bval(4 * g + 2 + h)};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int it = 0; it < IT; ++it) acc[0][it] = mfma32(cur[it][s2], b[s2], acc[0][it]);
+    };
+    float fa[IT][KH], fb[IT][KH];
+    load_frag<IT, KH>(fa, wptr);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 1 < NS; g += 2) {
+      step(fa, fb, g);
+      step(fb, fa, g + 1);
+    }
+    if (g < NS) step(fa, fb, g);
   } else {
     // Weight fragments stream linearly through (chunk, tap); they are prefetched
     // one tap ahead into the other of two register sets (ping-pong, no copies)
@@ -1395,9 +1428,19 @@ __global__ void pack_conv_kernel(const float* __restrict__ w, T* __restrict__ ds
   const int chunk = order == 0 ? outer : inner;
   const int tap = order == 0 ? inner : outer;
   const int o = cb * IT * 32 + it * 32 + (lane & 31);
-  const int c = chunk * CC + (lane >> 5) * KH + s;
+  int c = chunk * CC + (lane >> 5) * KH + s;
+  int tp = tap;
+  if (CC == 4) {
+    // C <= 4 input channels (RGB), packed K: slot (step g = tap, s) of lane half h holds the (tap, channel)
+    // pair f = 4g + 2s + h of the dense list f = tap*C + channel (zero past KK*C): no zero-padded 4th
+    // channel, ceil(KK*C/4) steps instead of KK (conv_down_kernel's fp32 CC = 4 main loop)
+    const int f = 4 * tap + 2 * s + (lane >> 5);
+    tp = f / C;
+    c = f - tp * C;
+    if (tp >= KK) c = C;  // past the list: zero
+  }
   float v = 0.f;
-  const int wt = flip ? KK - 1 - tap : tap;  // flip: spatially reversed kernel (dgrad of a stride-1 conv)
+  const int wt = flip ? KK - 1 - tp : tp;  // flip: spatially reversed kernel (dgrad of a stride-1 conv)
   if (o < O && c < C) v = w[o * so + c * sc + (wt / KS) * KS + (wt % KS)];
   dst[i] = (T)v;
 }
