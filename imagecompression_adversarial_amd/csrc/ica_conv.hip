@@ -1169,18 +1169,19 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
 // output channels to a 32-row MFMA tile (10.7x waste).  Instead:
 //   Z[(co,ky,kx)][pixel] = sum_ci W[ci][co][ky][kx] * x[ci][pixel]   (75 x Cin dense GEMM)
 //   out[co][2a+py][2b+px] = sum_{ky=py, kx=px (mod 2)} Z[(co,ky,kx)][a+dy, b+dx]
-// The block owns a 6x32 input-pixel tile; Z is computed for its 8x34 halo
-// tile into LDS (75 x 272 floats = 81600 B, so two blocks share a CU's 160 KB and one block's Z GEMM
+// The block owns a 5x32 input-pixel tile; Z is computed for its 7x34 halo
+// tile into LDS (75 x 238 floats = 71400 B, so two blocks share a CU's 160 KB and one block's Z GEMM
 // overlaps the other's gather and loads; the 8x32 tile's 102 KB Z allowed one block per CU, whose
-// phases then ran back to back), then each thread of the first 6 rows gathers the 12 outputs of one
-// input pixel.  Weight fragments packed [it(3)][chunk][lane][8] with row
+// phases then ran back to back).  The 238 halo pixels are 8 MFMA column tiles, 2 per wave (6 rows:
+// 9 tiles, 3/2/2/2; fp32 1.21 -> 1.19 ms).  Then each thread of the first 5 rows gathers the 12 outputs
+// of one input pixel.  Weight fragments packed [it(3)][chunk][lane][8] with row
 // o = it*32 + (lane&31) = co*25 + ky*5 + kx.
 // --------------------------------------------------------------------------
 #ifndef ICA_T3_TH
-#define ICA_T3_TH 6
+#define ICA_T3_TH 5
 #endif
-constexpr int T3_TH = ICA_T3_TH, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 272
-constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                                // 9
+constexpr int T3_TH = ICA_T3_TH, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 238
+constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                                // 8
 constexpr int T3_NCH_BF = 8;  // bf16 up-front-load path: Cin = 128
 constexpr int T3_BLOCKS = (2 * T3_ROWS * T3_NPX * 4 <= 160 * 1024) ? 2 : 1;
 
@@ -1204,7 +1205,7 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
     if (nch == T3_NCH_BF) {
       // bf16, Cin = 128 (the N = 128 models): the Z GEMM is latency-bound at one block per CU (the 102 KB Z
       // tile), so every load of the block is issued up front: all 24 weight fragments (once per block, L2) and
-      // the 8 chunks of each of this wave's (<= 3) pixel tiles (HBM, buffer loads with 32-bit offsets;
+      // the 8 chunks of each of this wave's (<= 2) pixel tiles (HBM, buffer loads with 32-bit offsets;
       // out-of-image pixels read past the descriptor and get zeros), then the tiles' MFMAs and Z stores.
       constexpr int MJ = (T3_JT + 3) / 4;
       const bf16x8* wl = reinterpret_cast<const bf16x8*>(p.wp) + lane;

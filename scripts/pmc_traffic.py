@@ -39,7 +39,7 @@ def up(epi, Hin, Win, Cout, it):
 
 
 def up3(Hin, Win):
-    return f"void conv_up3_kernel<{BF}>", -(-Win // 32) * -(-Hin // 6) * B * 256   # 6x32 input tiles
+    return f"void conv_up3_kernel<{BF}>", -(-Win // 32) * -(-Hin // 5) * B * 256   # 5x32 input tiles
 
 
 N, M = 128, 192
