@@ -4,8 +4,10 @@
 bf16-operand MFMA conv path (8 tiles per GPU, target = a second synthetic image, ROI = the centre box).
 
 One "step" = one attack_rd.attack_ iteration over the per-GPU batch: L-inf box
-+ input clamp, g_a + g_s forward, loss, g_s + g_a input-gradient backward, Adam
-on the noise (attack_rd.py:506-559) — every kernel on HIP, inputs resident in HBM.
++ input clamp, per-image branch (loss_i > -noise: input loss only, attack_rd.py:334-338), g_a + g_s forward,
+loss, g_s + g_a input-gradient backward for the images in the network branch (compacted sub-batch), Adam
+on the noise (attack_rd.py:506-559) — every kernel on HIP, inputs resident in HBM.  The line carries the
+branch census of the timed steps and (N = 1, hyperprior) of one whole 1001-step run with its wall time.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, weak scaling)
@@ -53,47 +55,78 @@ def layer_flops(tag, N, M, H, W, B):
     return 2.0 * macs * B
 
 
-def cpu_baseline(H, W, quality, seconds, model="hyper"):
-    """The CPU oracle (PyTorch-CPU fp32 restatement, kind 'port') timed on this host:
-    one reference attack step on ONE image, with weight gradients computed as the
-    reference does (params require grad), bounded to ~`seconds` of CPU work."""
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(H, W, quality, seconds, model="hyper", big_batch=32):
+    """The CPU oracle (PyTorch-CPU fp32 restatement, kind 'port') timed on this host, bounded to ~`seconds` of
+    CPU work per variant:
+      * value: one reference attack step on ONE image (the reference attacks one image per call,
+        attack_rd.py:646-670), weight gradients computed as the reference does (params require grad);
+      * variants: the same step without the unused weight gradients (dgrad only), and one step of a
+        ``big_batch``-image batch (the GPU workload's per-GPU batch) with weight gradients."""
     from oracle import codec
     # the box's CPU share (OMP_NUM_THREADS is set to it there); never oversubscribe
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0)))))
     P = codec.init_params(model, quality, seed=0)
-    for v in P.values():
-        v.requires_grad_(True)
-    g = torch.Generator().manual_seed(0)
-    im_s = torch.rand((1, 3, H, W), generator=g)
-    with torch.no_grad():
-        os_ = torch.clamp(codec.forward(P, im_s, model)["x_hat"], 0, 1)
-    noise = torch.zeros_like(im_s).requires_grad_(True)
-    opt = torch.optim.Adam([noise], lr=0.01)
     eps = 16 / 255.0
 
-    def one():
-        nc = codec.bound01(noise, -eps, eps)
-        im_in = codec.bound01(im_s + nc)
-        li = torch.mean((im_s - im_in) ** 2)
-        o = codec.bound01(codec.transforms(P, im_in, model))
-        loss = 1.0 - torch.mean((os_ - o) ** 2) if li <= 1e-4 else li
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
+    def make(B, wgrad):
+        for v in P.values():
+            v.requires_grad_(wgrad)
+        g = torch.Generator().manual_seed(0)
+        im_s = torch.rand((B, 3, H, W), generator=g)
+        with torch.no_grad():
+            os_ = torch.clamp(codec.forward(P, im_s[:1], model)["x_hat"], 0, 1).expand(B, -1, -1, -1)
+        noise = torch.zeros_like(im_s).requires_grad_(True)
+        opt = torch.optim.Adam([noise], lr=0.01)
 
-    one()
-    t0 = time.perf_counter()
-    n = 0
-    while True:
+        def one():
+            nc = codec.bound01(noise, -eps, eps)
+            im_in = codec.bound01(im_s + nc)
+            li = torch.mean((im_s - im_in) ** 2)
+            o = codec.bound01(codec.transforms(P, im_in, model))
+            loss = 1.0 - torch.mean((os_ - o) ** 2) if li <= 1e-4 else li
+            opt.zero_grad()
+            for v in P.values():
+                v.grad = None
+            loss.backward()
+            opt.step()
+        return one
+
+    def timed(one, B, budget, max_steps=50):
         one()
-        n += 1
-        el = time.perf_counter() - t0
-        if el > seconds or n >= 50:
-            break
-    return {"value": n / el, "unit": "attack-step·images/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+        t0 = time.perf_counter()
+        n = 0
+        while True:
+            one()
+            n += 1
+            el = time.perf_counter() - t0
+            if el > budget or n >= max_steps:
+                break
+        return B * n / el, n, el
+
+    v1, n1, e1 = timed(make(1, True), 1, seconds)
+    vd, nd, ed = timed(make(1, False), 1, seconds * 0.6)
+    one_b = make(big_batch, True)
+    t0 = time.perf_counter()
+    one_b()
+    eb = time.perf_counter() - t0
+    vb = big_batch / eb
+    return {"value": v1, "unit": "attack-step·images/s", "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": _cpu_model(),
             "sample": f"oracle attack step (fwd+bwd incl. weight grads as the reference), 1 image {W}x{H}, "
-                      f"{model} q{quality}, {n} timed steps after 1 warm-up ({el:.1f} s)"}
+                      f"{model} q{quality}, {n1} timed steps after 1 warm-up ({e1:.1f} s)",
+            "variants": {"b1_dgrad_only": {"value": vd, "sample": f"{nd} steps ({ed:.1f} s), no weight grads"},
+                         f"b{big_batch}_with_wgrad": {"value": vb,
+                                                      "sample": f"1 step of {big_batch} images ({eb:.1f} s)"}}}
 
 
 def _bf16_tags(kern):
@@ -125,9 +158,14 @@ def main():
                          "5 targeted ROI hyper q3 2048x2048 bf16")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-run", dest="full_run", type=int, default=None,
+                    help="1: also run the whole 1001-step loop once (wall time + branch census of the full run); "
+                         "default 1 for the hyperprior configs at N = 1, 0 for cheng2020 (~7 min)")
     args = ap.parse_args()
 
     roi_mode = False
+    if args.full_run is None:
+        args.full_run = int(args.config != 3 and args.model != "cheng2020")
     if args.config == 3:
         args.model = "cheng2020"
     elif args.config == 5:
@@ -190,6 +228,7 @@ def main():
         dist.barrier()
     K.EVENT_HOOK = {}
     K.FLOPS_HOOK = {}
+    exp0 = loop.expensive_image_steps()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
@@ -199,27 +238,31 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     hook, K.EVENT_HOOK = K.EVENT_HOOK, None
+    exp_steps = loop.expensive_image_steps() - exp0   # image-steps of the timed window that ran the network
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    # per-kernel average durations (HIP events on the launch stream)
-    per_tag = {tag: sum(a.elapsed_time(b) for a, b in evs) / len(evs) for tag, evs in hook.items()}
-    dom = max(per_tag, key=lambda t: per_tag[t] * len(hook[t]))
-    dom_ms = per_tag[dom]
-    if model == "cheng2020":   # per-launch algorithmic FLOPs recorded by hip_ops.conv_ex
-        flops_of = dict(K.FLOPS_HOOK)
+    # per-kernel durations (HIP events on the launch stream) and algorithmic FLOPs of every launch: a launch
+    # covers the images of its (compacted) batch, so the FLOPs are per-image FLOPs x the launch's images
+    if model == "cheng2020":   # per-image algorithmic FLOPs recorded by hip_ops.conv_ex
+        flops_img = dict(K.FLOPS_HOOK)
     else:
-        flops_of = {t: layer_flops(t, N, M, H, W, B) for t in per_tag}
-    dom_flops = flops_of[dom]
-    achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+        flops_img = {t: layer_flops(t, N, M, H, W, 1) for t in hook}
+    tot_ms = {tag: sum(a.elapsed_time(b) for a, b, _ in evs) for tag, evs in hook.items()}
+    tot_fl = {tag: sum(flops_img[tag] * n for _, _, n in evs) for tag, evs in hook.items()}
+    per_tag = {tag: tot_ms[tag] / len(hook[tag]) for tag in hook}
+    dom = max(tot_ms, key=tot_ms.get) if tot_ms else None
+    dom_ms = per_tag[dom] if dom else 0.0
+    dom_flops = tot_fl[dom] / len(hook[dom]) if dom else 0.0
+    achieved = tot_fl[dom] / (tot_ms[dom] * 1e-3) / 1e12 if dom else 0.0
     peak = BF16_MFMA_PEAK_TFLOPS if (args.precision == "bf16" and dom in _bf16_tags(kern)) else FP32_MFMA_PEAK_TFLOPS
     # HBM bytes per launch of the dominant kernel from the committed PMC passes of the same shapes
     # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)
     traffic = None
     tfile = None
-    if args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32):
+    if args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "hyper":
         tfile = "pmc_traffic.json"
     elif args.precision == "bf16" and (H, W, B) == (2048, 2048, 8):
         tfile = "pmc_traffic_c5.json"
@@ -229,10 +272,27 @@ def main():
             traffic = json.load(open(tf)).get(dom)
         except Exception:
             traffic = None
-    # network FLOPs of one step (every step of this loop takes the expensive branch: loss_i starts at 0)
-    total_flops = sum(flops_of[t] * len(hook[t]) for t in per_tag) / args.steps
+    # network FLOPs per timed step, weighted by the branches actually taken (a cheap-branch
+    # image-step runs no network and counts 0): the launches only covered the expensive images
+    total_flops = sum(tot_fl.values()) / args.steps
     ms_step = el / args.steps * 1e3
     value = B * world * args.steps / el
+
+    # the whole 1001-step loop once (N == 1): wall time, img-step/s and the branch census of the full run
+    full = None
+    if world == 1 and args.full_run:
+        loop2 = AttackLoop(kern, im_s, steps=1001, **roi_kw)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(1001):
+            loop2.step(i)
+        torch.cuda.synchronize()
+        fe = time.perf_counter() - t1
+        fx = loop2.expensive_image_steps()
+        full = {"steps": 1001, "wall_s": round(fe, 3), "value": round(B * 1001 / fe, 3),
+                "expensive_image_steps": fx, "image_steps": B * 1001,
+                "expensive_frac": round(fx / (B * 1001), 4)}
+        del loop2
 
     if rank == 0:
         cpu = None
@@ -260,6 +320,9 @@ def main():
                          "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
+            "branch_census": {"expensive_image_steps": exp_steps, "image_steps": B * args.steps,
+                              "expensive_frac": round(exp_steps / (B * args.steps), 4)},
+            "full_run": full,
             "step_gflop_per_image": round(total_flops / B / 1e9, 2),
             "step_tflops": round(total_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 /

@@ -138,6 +138,15 @@ class AttackLoop:
         self.im_in = torch.empty_like(self.im_s)
         self.lrs = _lr_table(steps, lr)
         self.t = 0
+        # branch compaction (attack_rd.py:334: the network runs only for images with loss_i <= -noise):
+        # per step one device->host read of the expensive-image list, then g_a/g_s on that sub-batch only.
+        # census[b] counts image b's cheap-branch steps (device-side, no sync).
+        self.compact = True
+        self.sel = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        self.gpos = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.sel_host = torch.zeros(B + 1, dtype=torch.int32).pin_memory() if dev.type == "cuda" else None
+        self.census = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.steps_done = 0
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
         self.output_s, self.bpp_ori = eval_forward(kern, self.im_s, clamp)
         self.output_s4 = None
@@ -158,28 +167,56 @@ class AttackLoop:
         step_size = self.lrs[i] / bc1
         return float(bc2 ** 0.5), float(-step_size)
 
-    def network_grad(self):
-        """x_hat = g_s(g_a(im_in)); grad4 = d loss_o / d im_in (nChw4c, C=3)."""
+    def _select(self):
+        """Expensive images of this step: (E, idx) with idx the sorted host list (None when E == B)."""
+        B = self.B
+        if not self.compact:
+            return B, None
+        call("ica_branch_select", ptr(self.loss_i), self.thr, B, ptr(self.sel), ptr(self.gpos), stream())
+        self.sel_host.copy_(self.sel, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        E = int(self.sel_host[0])
+        if E == B:
+            return B, None
+        return E, self.sel[1:1 + E]
+
+    def _gather(self, x, idx, E):
+        if idx is None:
+            return x
+        per = x[0].numel()
+        out = torch.empty((E,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        call("ica_gather_images", ptr(x), ptr(out), ptr(idx), E, per, stream())
+        return out
+
+    def network_grad(self, idx=None, E=None):
+        """x_hat = g_s(g_a(im_in)); d loss_o / d im_in (nChw4c, C=3) for the images idx (all when None): the
+        expensive-branch work of attack_our (attack_rd.py:340-379), on a compacted sub-batch."""
         kern = self.kern
-        B, H, W = self.B, self.H, self.W
-        y4, sa = kern.g_a(self.im_in4, save=True)
+        H, W = self.H, self.W
+        Bn = self.B if idx is None else E
+        im4 = self._gather(self.im_in4, idx, Bn)
+        out_s = self._gather(self.output_s, idx, Bn)
+        grad4, part = self.grad4[:Bn], self.part[:Bn * K.blocks_per_image()]
+        y4, sa = kern.g_a(im4, save=True)
+        del im4
         xh4, ss = kern.g_s(y4, save=True)
         del y4
         if self.roi is not None:
             x0, x1, y0, y1, _, _, wot, wob = self.roi
-            call("ica_roi_loss", ptr(xh4), ptr(self.output_s), ptr(self.output_t), ptr(self.grad4), ptr(self.part),
-                 B, H, W, x0, x1, y0, y1, wot, wob, int(self.clamp), stream())
+            out_t = self._gather(self.output_t, idx, Bn)
+            call("ica_roi_loss", ptr(xh4), ptr(out_s), ptr(out_t), ptr(grad4), ptr(part),
+                 Bn, H, W, x0, x1, y0, y1, wot, wob, int(self.clamp), stream())
         elif self.metric == "L2":
-            call("ica_attack_loss", ptr(xh4), ptr(self.output_s), ptr(self.grad4), ptr(self.part), B, H, W,
+            call("ica_attack_loss", ptr(xh4), ptr(out_s), ptr(grad4), ptr(part), Bn, H, W,
                  self.gscale, int(self.clamp), 0, stream())
         else:
             # loss_o = ms_ssim(out, output_s) per image (attack_rd.py:362)
-            out = torch.empty_like(self.im_s)
-            call("ica_nc4_bound_to_nchw", ptr(xh4), ptr(out), B, H, W, int(self.clamp), stream())
-            ones = torch.full((B,), self.dval, device=out.device)
-            _, gout, _ = MS.ms_ssim_value_and_grad(out, self.output_s, ones)
-            call("ica_bound_bwd_nc4", ptr(xh4), ptr(gout), ptr(self.grad4), B, H, W, int(self.clamp), stream())
-        gy4 = kern.g_s_backward(self.grad4, ss)
+            out = torch.empty_like(out_s)
+            call("ica_nc4_bound_to_nchw", ptr(xh4), ptr(out), Bn, H, W, int(self.clamp), stream())
+            ones = torch.full((Bn,), self.dval, device=out.device)
+            _, gout, _ = MS.ms_ssim_value_and_grad(out, out_s, ones)
+            call("ica_bound_bwd_nc4", ptr(xh4), ptr(gout), ptr(grad4), Bn, H, W, int(self.clamp), stream())
+        gy4 = kern.g_s_backward(grad4, ss)
         del ss, xh4
         return kern.g_a_backward(gy4, sa)
 
@@ -192,9 +229,10 @@ class AttackLoop:
         K.reduce_rows(self.part, B, self.invN, out=self.loss_i)
         if self.coupled:
             D.couple_loss_i(self.loss_i, self.B_global, self.group)
-        gx4 = self.network_grad()
+        E, idx = self._select()
+        gx4 = self.network_grad(idx, E) if E > 0 else None
         cheap_grad = None
-        if self.metric == "ms-ssim":
+        if self.metric == "ms-ssim" and E < B:
             # cheap branch loss = 1 - ms_ssim(im_s, im_in): d/d im_in = -dMS/dY
             im_in = torch.empty_like(self.im_s)
             call("ica_nc4_bound_to_nchw", ptr(self.im_in4), ptr(im_in), B, H, W, 0, stream())
@@ -203,7 +241,9 @@ class AttackLoop:
         bc2s, neg_step = self._adam_scalars(i)
         call("ica_attack_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(cheap_grad),
              ptr(self.m), ptr(self.v), ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr,
-             self.gscale, bc2s, neg_step, ptr(self.branch), stream())
+             self.gscale, bc2s, neg_step, ptr(self.branch), ptr(self.gpos if idx is not None else None),
+             ptr(self.census), stream())
+        self.steps_done += 1
         if census:
             return self.branch.tolist()
         return None
@@ -214,14 +254,21 @@ class AttackLoop:
         call("ica_roi_prologue", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
              self.eps, x0, x1, y0, y1, wit, wib, stream())
         K.reduce_rows(self.part, B, 1.0, out=self.loss_i)
-        gx4 = self.network_grad()
+        E, idx = self._select()
+        gx4 = self.network_grad(idx, E) if E > 0 else None
         bc2s, neg_step = self._adam_scalars(i)
         call("ica_roi_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(self.m), ptr(self.v),
              ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr, bc2s, neg_step,
-             ptr(self.branch), x0, x1, y0, y1, wit, wib, stream())
+             ptr(self.branch), x0, x1, y0, y1, wit, wib, ptr(self.gpos if idx is not None else None),
+             ptr(self.census), stream())
+        self.steps_done += 1
         if census:
             return self.branch.tolist()
         return None
+
+    def expensive_image_steps(self):
+        """Image-steps that ran the network so far (B * steps - the device census of cheap steps)."""
+        return self.B * self.steps_done - int(self.census.sum())
 
     def run(self, record=False):
         branches = []

@@ -11,6 +11,9 @@ main          attack_rd.py:706-715
 Differences from the reference, all deliberate and documented:
   * ``--batch B`` attacks B same-size images per launch with per-image semantics
     (bit-identical to B separate runs; tests/test_gpu_attack.py).
+  * ``python -m torch.distributed.run --nproc-per-node N -m imagecompression_adversarial_amd.attack_rd ...``
+    shards the sorted image list over N ranks (one GPU each, no collective on the attack path); rank 0
+    prints the per-image lines in reference order and the AVG line.
   * A ``vi`` of None (mse_out == 0, reference warning at self_ensemble.py:244)
     does not crash the random-restart selection (reference compares None > float).
   * ``-p/--pad`` and ``--defend`` are not supported (``--defend`` crashes inside the
@@ -21,7 +24,10 @@ Differences from the reference, all deliberate and documented:
 """
 from __future__ import annotations
 
+import contextlib
+import io
 import math
+import os
 import time
 from glob import glob
 
@@ -81,12 +87,39 @@ def _target_tensor(spec, im_s):
 
 
 def _sources(spec):
-    """Glob of image files, or synthetic:<B>x<H>x<W> (seeded torch.rand images)."""
+    """Glob of image files (sorted, attack_rd.py:648), or synthetic:<B>x<H>x<W> (seeded torch.rand images)."""
     if spec.startswith("synthetic:"):
         B, H, W = (int(v) for v in spec.split(":", 1)[1].split("x"))
         g = torch.Generator().manual_seed(0)
         return [(f"synthetic_{i}", torch.rand((1, 3, H, W), generator=g), H, W) for i in range(B)]
     return [(f, None, None, None) for f in sorted(glob(spec))]
+
+
+def _padded_shape(item, padding=64):
+    """NCHW shape coder.read_image will produce (zero-padded to a multiple of 64), from the PNG header only."""
+    name, t, _, _ = item
+    if t is not None:
+        return tuple(t.shape)
+    from PIL import Image
+    with Image.open(name) as im:
+        W, H = im.size
+    return (1, 3, padding * math.ceil(H / padding), padding * math.ceil(W / padding))
+
+
+def _groups(items, batch):
+    """Consecutive runs of same-padded-size images, at most ``batch`` per launch (per-image semantics: the
+    grouping changes nothing numerically, only how many images share one set of kernel launches)."""
+    groups, cur, cur_shape = [], [], None
+    for it in items:
+        shape = _padded_shape(it)
+        if cur and (len(cur) >= max(batch, 1) or shape != cur_shape):
+            groups.append(cur)
+            cur = []
+        cur.append(it)
+        cur_shape = shape
+    if cur:
+        groups.append(cur)
+    return groups
 
 
 class attacker:
@@ -130,23 +163,11 @@ class attacker:
         return out
 
 
-def batch_attack(args):
-    myattacker = attacker(args)
-    items = _sources(args.source)
-    # group same-size images (per-image semantics: grouping changes nothing numerically)
-    groups, cur = [], []
-    for it in items:
-        shape = None if it[1] is None else tuple(it[1].shape)
-        if cur and (len(cur) >= max(args.batch, 1) or shape is None or cur[-1][0] != shape):
-            groups.append(cur)
-            cur = []
-        cur.append((shape, it))
-    if cur:
-        groups.append(cur)
-    bpp_ori_, bpp_, vi_, vi_anchor_, vi_msim_, t_ = 0.0, 0.0, 0.0, 0.0, 0.0, 0.0
-    n_done = 0
-    for grp in groups:
-        batch = [it for _, it in grp]
+def _attack_items(myattacker, items, args):
+    """Attack ``items`` group by group; returns one (name, bpp_ori, bpp, vi_results, seconds) per image, in
+    order.  -random R: R restarts, the best vi kept per image (attack_rd.py:657-664)."""
+    out = []
+    for batch in _groups(items, args.batch):
         start = time.time()
         best = [None] * len(batch)
         for _ in range(args.random):
@@ -155,21 +176,69 @@ def batch_attack(args):
                 vb = r[2]["vi"] if r[2]["vi"] is not None else -float("inf")
                 if best[b] is None or vb > (best[b][2]["vi"] if best[b][2]["vi"] is not None else -float("inf")):
                     best[b] = r
-        end = time.time()
+        per_t = (time.time() - start) / len(batch)
         for b, (bpp_ori, bpp, vi_results) in enumerate(best):
-            per_t = (end - start) / len(batch)
-            print(batch[b][0], bpp_ori, bpp, vi_results["vi"], vi_results["vi_msim"], "Time:", per_t)
-            bpp_ori_ += bpp_ori
-            bpp_ += bpp
-            vi_ += vi_results["vi"] if vi_results["vi"] is not None else 0.0
-            vi_anchor_ += vi_results["vi_anchor"] if vi_results["vi_anchor"] is not None else 0.0
-            # reference quirk kept: vi_msim_ starts at 0.0 (falsy) so the AVG vi_msim is None
-            if vi_results["vi_msim"] and vi_msim_:
-                vi_msim_ += vi_results["vi_msim"]
-            else:
-                vi_msim_ = None
-            t_ += per_t
-            n_done += 1
+            out.append((batch[b][0], bpp_ori, bpp, vi_results, per_t))
+    return out
+
+
+def _dist_setup(args):
+    """torchrun launch (WORLD_SIZE > 1): one process per GPU, -device becomes this rank's GPU.  The process
+    group carries only the final result gather (no collective on the attack path)."""
+    from . import dist as D
+    world, _, local = D.env_world()
+    if world <= 1:
+        return 0, 1, None
+    backend = os.environ.get("ICA_DIST_BACKEND")  # default: RCCL on a GPU host, gloo on CPU
+    if str(args.device).startswith(("cuda", "hip")):
+        ndev = torch.cuda.device_count()
+        args.device = f"cuda:{local % max(ndev, 1)}"
+        if backend is None and ndev >= world:
+            backend = "nccl"
+    rank, world, group = D.init_from_env(backend or "gloo")
+    return rank, world, group
+
+
+def batch_attack(args):
+    """attack_rd.batch_attack (attack_rd.py:646-699).  Under torchrun the sorted image list is split into
+    contiguous per-rank shards (dist.shard_range); every rank attacks its shard with no collective, the
+    per-image result tuples are gathered to rank 0 once at the end, and rank 0 prints the reference's
+    per-image lines (:670) in reference order and the AVG line (:688)."""
+    from . import dist as D
+    rank, world, group = _dist_setup(args)
+    if rank == 0:
+        myattacker = attacker(args)
+    else:   # settings banners once, from rank 0 (the output matches a one-process run line for line)
+        with contextlib.redirect_stdout(io.StringIO()):
+            myattacker = attacker(args)
+    items = _sources(args.source)
+    shard = D.shard_range(len(items), rank, world)
+    results = _attack_items(myattacker, [items[i] for i in shard], args)
+    if world > 1:
+        import torch.distributed as tdist
+        gathered = [None] * world if rank == 0 else None
+        # names of synthetic items are strings, tensors are not shipped: only the printed numbers travel
+        tdist.gather_object(results, gathered, dst=0, group=group)
+        if rank != 0:
+            tdist.barrier(group=group)
+            return None
+        results = [r for part in gathered for r in part]
+        tdist.barrier(group=group)
+    bpp_ori_, bpp_, vi_, vi_anchor_, vi_msim_, t_ = 0.0, 0.0, 0.0, 0.0, 0.0, 0.0
+    n_done = 0
+    for name, bpp_ori, bpp, vi_results, per_t in results:
+        print(name, bpp_ori, bpp, vi_results["vi"], vi_results["vi_msim"], "Time:", per_t)
+        bpp_ori_ += bpp_ori
+        bpp_ += bpp
+        vi_ += vi_results["vi"] if vi_results["vi"] is not None else 0.0
+        vi_anchor_ += vi_results["vi_anchor"] if vi_results["vi_anchor"] is not None else 0.0
+        # reference quirk kept: vi_msim_ starts at 0.0 (falsy) so the AVG vi_msim is None (SURVEY App. B)
+        if vi_results["vi_msim"] and vi_msim_:
+            vi_msim_ += vi_results["vi_msim"]
+        else:
+            vi_msim_ = None
+        t_ += per_t
+        n_done += 1
     num_im = max(n_done, 1)
     vi_msim = vi_msim_ / num_im if vi_msim_ else None
     bpp_ori, bpp, vi, vi_anchor, t = bpp_ori_ / num_im, bpp_ / num_im, vi_ / num_im, vi_anchor_ / num_im, t_ / num_im
@@ -191,3 +260,6 @@ def main(args):
 
 if __name__ == "__main__":
     main(coder.config().parse_args())
+    import torch.distributed as _tdist
+    if _tdist.is_initialized():
+        _tdist.destroy_process_group()

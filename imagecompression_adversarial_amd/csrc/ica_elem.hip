@@ -224,19 +224,27 @@ __global__ void roi_loss_kernel(const float* __restrict__ xhat4, const float* __
 // denom = sqrt(v)/bc2s + eps; p = p + neg_step*(m/denom)
 // ROI (targeted / masked attack): the cheap-branch input loss is the box-weighted mean, so the
 // per-element weight w_in(pixel) replaces invN (same op order: t = w*(s - ii), g = -(t + t)).
+// gpos (optional): row of image b in gnet4 when the network ran on a compacted sub-batch of the expensive
+// images (ica_branch_select); null = gnet4 is indexed by b.  census (optional): census[b] += cheap, the
+// per-image count of cheap-branch steps (network FLOPs count only the expensive image-steps).
 template <bool ROI>
 __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __restrict__ im_s,
                                    const float* __restrict__ gnet4, const float* __restrict__ loss_i,
                                    const float* __restrict__ cheap_grad, float* __restrict__ m,
                                    float* __restrict__ v, float* __restrict__ im_in_out, long HW, float eps,
                                    float thr, float invN, float bc2s, float neg_step, int* __restrict__ branch,
-                                   RoiBox roi, long W) {
+                                   RoiBox roi, long W, const int* __restrict__ gpos, int* __restrict__ census) {
   const int b = blockIdx.y;
   const bool cheap = loss_i[b] > thr;
-  if (branch && blockIdx.x == 0 && threadIdx.x == 0) branch[b] = cheap ? 1 : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (branch) branch[b] = cheap ? 1 : 0;
+    if (census) census[b] += cheap ? 1 : 0;
+  }
   const long off = (long)b * 3 * HW;
+  const long grow = cheap ? 0 : (gpos ? gpos[b] : b);   // the network gradient is read only when used
   for (long pix = (long)blockIdx.x * 256 + threadIdx.x; pix < HW; pix += (long)gridDim.x * 256) {
-    const f32x4 gn = ld4(gnet4 + ((long)b * HW + pix) * 4);
+    f32x4 gn = {0.f, 0.f, 0.f, 0.f};
+    if (!cheap) gn = ld4(gnet4 + (grow * HW + pix) * 4);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const long i = off + c * HW + pix;
@@ -277,6 +285,30 @@ __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __res
       noise[i] = fadd_rn(nz, fmul_rn(neg_step, fdiv_rn(mn, denom)));
     }
   }
+}
+
+// Branch compaction (attack_rd.py:334 decides per image whether the network runs at all).  One thread walks
+// the batch in order: idx[0..E) = the expensive images (loss_i <= thr), gpos[b] = their row in the compacted
+// sub-batch (-1 for cheap images), sel[0] = E.  The host reads sel (E + B ints) to size the sub-batch.
+__global__ void branch_select_kernel(const float* __restrict__ loss_i, float thr, int B, int* __restrict__ sel,
+                                     int* __restrict__ gpos) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int e = 0;
+  for (int b = 0; b < B; ++b) {
+    const bool cheap = loss_i[b] > thr;
+    gpos[b] = cheap ? -1 : e;
+    if (!cheap) sel[1 + e++] = b;
+  }
+  sel[0] = e;
+}
+
+// dst[r] = src[idx[r]] for r < E: whole images of `quads` 16-byte vectors each (grid.y = E).
+__global__ void gather_images_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                     const int* __restrict__ idx, long quads) {
+  const int r = blockIdx.y;
+  const f32x4* s = src + (long)idx[r] * quads;
+  f32x4* d = dst + (long)r * quads;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < quads; i += (long)gridDim.x * 256) d[i] = s[i];
 }
 
 // I-FGSM / MI-FGSM step (attack_ifgsm.py:348-362, 405-419), per image.
@@ -595,10 +627,10 @@ int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float*
 
 int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
                     float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
-                    float bc2s, float neg_step, int* branch, hipStream_t st) {
+                    float bc2s, float neg_step, int* branch, const int* gpos, int* census, hipStream_t st) {
   hipLaunchKernelGGL(attack_adam_kernel<false>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
                      loss_i, cheap_grad, m, v, im_in_out, (long)H * W, eps, thr, invN, bc2s, neg_step, branch,
-                     RoiBox{}, (long)W);
+                     RoiBox{}, (long)W, gpos, census);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -623,11 +655,29 @@ int ica_roi_loss(const float* xhat4, const float* out_s, const float* out_t, flo
 
 int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, float* m, float* v,
                  float* im_in_out, int B, int H, int W, float eps, float thr, float bc2s, float neg_step, int* branch,
-                 int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t st) {
+                 int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, const int* gpos, int* census,
+                 hipStream_t st) {
   const RoiBox roi{x0, x1, y0, y1, w_in_tar, w_in_bkg, 0.f, 0.f};
   hipLaunchKernelGGL(attack_adam_kernel<true>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
                      loss_i, nullptr, m, v, im_in_out, (long)H * W, eps, thr, 0.f, bc2s, neg_step, branch, roi,
-                     (long)W);
+                     (long)W, gpos, census);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_branch_select(const float* loss_i, float thr, int B, int* sel, int* gpos, hipStream_t st) {
+  hipLaunchKernelGGL(branch_select_kernel, dim3(1), dim3(64), 0, st, loss_i, thr, B, sel, gpos);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_gather_images(const float* src, float* dst, const int* idx, int E, long floats_per_image, hipStream_t st) {
+  if (E <= 0) return 0;
+  if (floats_per_image % 4) return (int)hipErrorInvalidValue;
+  const long quads = floats_per_image / 4;
+  const int gx = (int)((quads + 255) / 256 < 1024 ? (quads + 255) / 256 : 1024);
+  hipLaunchKernelGGL(gather_images_kernel, dim3(gx, E), dim3(256), 0, st, reinterpret_cast<const f32x4*>(src),
+                     reinterpret_cast<f32x4*>(dst), idx, quads);
   ICA_CHECK_LAUNCH();
   return 0;
 }

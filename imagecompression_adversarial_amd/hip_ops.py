@@ -24,25 +24,26 @@ GDN_BETA_BOUND = float((1e-6 + 2.0 ** -36) ** 0.5)  # NonNegativeParametrizer bo
 EVENT_HOOK = None
 
 
-def _ev_begin(tag):
+def _ev_begin(tag, n):
     if EVENT_HOOK is None or tag is None:
         return None
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    return (tag, e0)
+    return (tag, e0, n)
 
 
 def _ev_end(h, flops=None):
+    """EVENT_HOOK[tag] gets (start event, end event, images in the launch)."""
     if h is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        EVENT_HOOK.setdefault(h[0], []).append((h[1], e1))
+        EVENT_HOOK.setdefault(h[0], []).append((h[1], e1, h[2]))
         if flops is not None:
-            FLOPS_HOOK[h[0]] = flops
+            FLOPS_HOOK[h[0]] = flops / max(h[2], 1)
 
 
-# algorithmic FLOPs per tagged ica_conv_ex launch (filled while EVENT_HOOK is set): 2*MAC of the conv
-# (a transposed conv counts the MACs of the conv it differentiates) + the GDN channel GEMM if fused
+# algorithmic FLOPs PER IMAGE of each tagged ica_conv_ex launch (filled while EVENT_HOOK is set): 2*MAC of the
+# conv (a transposed conv counts the MACs of the conv it differentiates) + the GDN channel GEMM if fused
 FLOPS_HOOK = {}
 
 
@@ -266,7 +267,7 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     in_x = in_s = None
     if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
         in_x, in_s = saved
-    ev = _ev_begin(tag)
+    ev = _ev_begin(tag, N)
     call("ica_conv_down", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, KS, S, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
          ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), ptr(save_t), stream())
@@ -285,7 +286,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     if Cout == 3:
         if epi != EPI_BIAS:
             raise RuntimeError("conv_up to 3 channels supports the bias epilogue only")
-        ev = _ev_begin(tag)
+        ev = _ev_begin(tag, N)
         call("ica_conv_up3_bf16" if prec == PREC_BF16 else "ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
              Cin, H, W, stream())
         _ev_end(ev)
@@ -298,7 +299,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     in_x = in_s = None
     if epi in (EPI_GDN_BWD, EPI_IGDN_BWD):
         in_x, in_s = saved
-    ev = _ev_begin(tag)
+    ev = _ev_begin(tag, N)
     call("ica_conv_up", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, Cout, Ho, Wo, epi,
          ptr(None if gdn is None else (gdn.gpT if epi >= EPI_GDN_BWD else gdn.gp)),
          ptr(None if gdn is None else gdn.beta), None, ptr(ss), ptr(in_x), ptr(in_s), ptr(save_t), stream())
@@ -356,7 +357,7 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
                  ptr(save_s), ptr(in_x), ptr(in_s), ptr(save_t), ptr(res), ptr(mask), N, Cin, H, W, Cout, Ho, Wo,
                  kind, KS, S, epi, it, fill_mode, int(bool(ps)), int(prec))
     import ctypes
-    ev = _ev_begin(tag)
+    ev = _ev_begin(tag, N)
     call("ica_conv_ex", ctypes.c_void_p(ctypes.addressof(a)), stream())
     if ev is not None:
         px = N * (H * W if kind == 1 else Ho * Wo)

@@ -352,6 +352,9 @@ class DefendedAttackLoop(AttackLoop):
         if kw.get("att_metric", "L2") != "L2" or kw.get("target") is not None or kw.get("coupled"):
             raise NotImplementedError("self_ensemble's attack is the per-image L2 attack")
         super().__init__(kern, im_s, **kw)
+        # the defences draw their noise for the whole batch each step (the reference's draw shapes), so the
+        # network runs on the full batch here: no branch compaction
+        self.compact = False
         self.method, self.noise_fn = method, noise_fn
         self.resize = _ResizePair(self.H, self.W) if method == "resize" else None
         self.best_hist = []   # per step: the best variant index of each image (ensemble)
@@ -365,7 +368,8 @@ class DefendedAttackLoop(AttackLoop):
         self._i = i
         return super().step(i, record_im_in, census)
 
-    def network_grad(self):
+    def network_grad(self, idx=None, E=None):
+        assert idx is None, "DefendedAttackLoop runs the network on the full batch"
         if self.method == "ensemble":
             return self._grad_ensemble()
         return self._grad_noisy()

@@ -186,7 +186,14 @@ int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float*
 /* Per-image branch (loss_i[b] > thr), bounds backward, torch-Adam step on noise/m/v (in place). */
 int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
                     float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
-                    float bc2s, float neg_step, int* branch, hipStream_t stream);
+                    float bc2s, float neg_step, int* branch, const int* gpos, int* census, hipStream_t stream);
+/* Branch compaction: sel[0] = E = #images with loss_i <= thr (the network branch, attack_rd.py:334), sel[1..E] =
+ * their indexes in order, gpos[b] = row of image b in the compacted sub-batch (-1: cheap branch, no network).
+ * ica_attack_adam / ica_roi_adam read the network gradient of image b from row gpos[b] (gpos null: row b) and,
+ * with census non-null, add the cheap flag into census[b] (per-image count of cheap-branch steps). */
+int ica_branch_select(const float* loss_i, float thr, int B, int* sel, int* gpos, hipStream_t stream);
+/* dst[r] = src[idx[r]], r < E, whole images of floats_per_image floats (a multiple of 4). */
+int ica_gather_images(const float* src, float* dst, const int* idx, int E, long floats_per_image, hipStream_t stream);
 /* Targeted / ROI attack (README "attack with ROI", attack_cv.py:153-163 mask box,
  * attack_data.py:202-226 target / masked losses; semantics fixed in DESIGN.md).  Box [y0,y1) x [x0,x1) is the
  * target region; w_* are the per-element weights of the masked means (1 / count, la_x / count).
@@ -199,7 +206,8 @@ int ica_roi_loss(const float* xhat4, const float* out_s, const float* out_t, flo
                  int W, int x0, int x1, int y0, int y1, float w_out_tar, float w_out_bkg, int clamp, hipStream_t stream);
 int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, float* m, float* v,
                  float* im_in_out, int B, int H, int W, float eps, float thr, float bc2s, float neg_step, int* branch,
-                 int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t stream);
+                 int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, const int* gpos, int* census,
+                 hipStream_t stream);
 int ica_ifgsm_step(float* x, const float* im_s, const float* grad4, float* gacc, const float* l1, int B, int H, int W,
                    float alpha, float eps, int momentum, hipStream_t stream);
 int ica_l1_partial(const float* g4, float* part, int B, int H, int W, hipStream_t stream);

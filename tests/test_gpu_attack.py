@@ -254,3 +254,28 @@ def test_quality6_n192_vs_oracle(model):
     ref = codec.forward(P, x, model)
     bref = torch.stack([codec.bpp({k: v[b:b + 1] for k, v in ref["likelihoods"].items()}, 64 * 128) for b in range(2)])
     assert torch.allclose(bpp.cpu(), bref, rtol=1e-4, atol=1e-5)
+
+
+def test_branch_compaction_bitexact():
+    """The network runs only on the images in the expensive branch (compacted sub-batch, attack_rd.py:334):
+    bit-identical to running it on the whole batch, with steps where the batch's images take different
+    branches; the device census counts the cheap image-steps."""
+    from imagecompression_adversarial_amd.attack import AttackLoop
+    from imagecompression_adversarial_amd.engine import CodecKernels
+    P = codec.perturb_params(codec.init_params("hyper", 1, seed=0), seed=1)
+    P["g_a.6.weight"] = P["g_a.6.weight"] * 40.0
+    kern = CodecKernels({k: v.to(DEV) for k, v in P.items()}, "hyper")
+    x = torch.cat([rnd((1, 3, 64, 96), 91), rnd((1, 3, 64, 96), 92) * 0.5, rnd((1, 3, 64, 96), 93)], 0).to(DEV)
+    loops, hist = [], []
+    for compact in (True, False):
+        loop = AttackLoop(kern, x, steps=30, noise_thr=1e-4)
+        loop.compact = compact
+        hist.append([loop.step(i, census=True) for i in range(30)])
+        loops.append(loop)
+    assert hist[0] == hist[1]
+    assert any(0 < sum(br) < 3 for br in hist[0]), hist[0]       # mixed-branch steps were exercised
+    assert torch.equal(loops[0].noise, loops[1].noise)
+    assert torch.equal(loops[0].m, loops[1].m) and torch.equal(loops[0].v, loops[1].v)
+    cheap = [sum(br[b] for br in hist[0]) for b in range(3)]
+    assert loops[0].census.tolist() == cheap
+    assert loops[0].expensive_image_steps() == 90 - sum(cheap)
