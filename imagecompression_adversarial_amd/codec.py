@@ -11,8 +11,10 @@ Replaces the un-vendored third-party surface the reference drives
 ``g_a`` / ``g_s`` are nn.Sequential containers (so parameters and indexing
 look like CompressAI's) whose forward runs the fused HIP chain as one
 autograd Function: forward saves the GDN activations, backward runs the fused
-dgrad chain.  Weight gradients are not produced on this path (the attack
-freezes the codec); see ``requires_grad`` note in DESIGN.md.
+dgrad chain and, when the bmshj2018 g_a / g_s parameters require grad, their
+weight / bias / GDN gradients on the HIP wgrad kernels.  The other transforms
+(h_a / h_s, cheng2020) raise when asked for parameter gradients; the full-model
+train step is train_engine.RDTrainer.
 """
 from __future__ import annotations
 
@@ -99,29 +101,57 @@ def _key(module: nn.Module):
 
 
 class _TransformFn(torch.autograd.Function):
+    """One fused HIP chain as an autograd node.  Backward: the input gradient, and, when the transform's
+    parameters require grad, their gradients from the HIP wgrad / GDN-parameter kernels (the bmshj2018
+    transforms; train_engine.analysis_backward / synthesis_backward)."""
+
     @staticmethod
     def forward(ctx, x, module, *params):
         ex = module._executor()
-        need = ctx.needs_input_grad[0]
-        out4, saved = ex.forward(K.to_nc4(x.detach().contiguous()), save=need)
-        ctx.ex, ctx.saved, ctx.cin = ex, saved, x.shape[1]
+        need_x = ctx.needs_input_grad[0]
+        need_w = any(ctx.needs_input_grad[2:])
+        if need_w and not module._wgrad_ok:
+            raise NotImplementedError(f"{type(module).__name__}: parameter gradients are computed for the bmshj2018 "
+                                      "g_a / g_s only; freeze this transform with requires_grad_(False)")
+        x4 = K.to_nc4(x.detach().contiguous())
+        out4, saved = ex.forward(x4, save=need_x or need_w)
+        ctx.ex, ctx.saved, ctx.cin, ctx.module = ex, saved, x.shape[1], module
+        ctx.x4 = x4 if need_w else None
+        ctx.need_x, ctx.need_w = need_x, need_w
         return K.from_nc4(out4, module.out_channels)
 
     @staticmethod
     def backward(ctx, gy):
-        gx4 = ctx.ex.backward(K.to_nc4(gy.contiguous()), ctx.saved)
-        ctx.saved = None
-        return (K.from_nc4(gx4, ctx.cin), None) + (None,) * (len(ctx.needs_input_grad) - 2)
+        from . import train_engine as T
+        g4 = K.to_nc4(gy.contiguous())
+        module, ex = ctx.module, ctx.ex
+        pgrads = (None,) * (len(ctx.needs_input_grad) - 2)
+        gx = None
+        if ctx.need_w:
+            named = list(module.named_parameters())
+            params = {n: p.detach() for n, p in named}
+            grads = {n: torch.zeros_like(p) for n, p in named}
+            if isinstance(module, AnalysisTransform):
+                gx4 = T.analysis_backward(ex, g4, ctx.x4, ctx.saved, params, grads, "", input_grad=ctx.need_x)
+            else:
+                gx4 = T.synthesis_backward(ex, g4, ctx.x4, ctx.saved, params, grads, "")
+            pgrads = tuple(grads[n] for n, _ in named)
+            if ctx.need_x:
+                gx = K.from_nc4(gx4, ctx.cin)
+        elif ctx.need_x:
+            gx = K.from_nc4(ex.backward(g4, ctx.saved), ctx.cin)
+        ctx.saved = ctx.x4 = None
+        return (gx, None) + pgrads
 
 
 class _FusedSequential(nn.Sequential):
     _exec_cls = None
+    _wgrad_ok = False   # parameter gradients through the module API (bmshj2018 g_a / g_s)
 
     def __init__(self, *layers):
         super().__init__(*layers)
         self._ex = None
         self._ex_key = None
-        self._warned = False
 
     def _executor(self):
         k = _key(self)
@@ -134,15 +164,12 @@ class _FusedSequential(nn.Sequential):
         if not torch.is_grad_enabled():
             out4, _ = self._executor().forward(K.to_nc4(x.detach().contiguous()), save=False)
             return K.from_nc4(out4, self.out_channels)
-        if not self._warned and any(p.requires_grad for p in self.parameters()):
-            self._warned = True
-            warnings.warn("codec weight gradients are not computed on the HIP attack path (input gradients "
-                          "only); freeze the codec with requires_grad_(False) to silence this", stacklevel=2)
         return _TransformFn.apply(x, self, *self.parameters())
 
 
 class AnalysisTransform(_FusedSequential):
     """g_a: conv(3,N)-GDN-conv(N,N)-GDN-conv(N,N)-GDN-conv(N,M) (CompressAI bmshj2018)."""
+    _wgrad_ok = True
 
     def __init__(self, N, M):
         super().__init__(conv(3, N), GDN(N), conv(N, N), GDN(N), conv(N, N), GDN(N), conv(N, M))
@@ -154,6 +181,7 @@ class AnalysisTransform(_FusedSequential):
 
 class SynthesisTransform(_FusedSequential):
     """g_s: deconv(M,N)-IGDN-deconv(N,N)-IGDN-deconv(N,N)-IGDN-deconv(N,3)."""
+    _wgrad_ok = True
 
     def __init__(self, N, M):
         super().__init__(deconv(M, N), GDN(N, inverse=True), deconv(N, N), GDN(N, inverse=True),
@@ -179,8 +207,10 @@ class _ForwardOnly(nn.Sequential):
 
     def forward(self, x):
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
-            if x.requires_grad:
-                raise NotImplementedError("hyperprior transforms are forward-only on the HIP path")
+            # no silent gradient hole: a caller that trains through the module API (train.py:349-362) must
+            # use the HIP trainer (train_engine.RDTrainer, train.py --adv), which covers these transforms
+            raise NotImplementedError(f"{type(self).__name__} is forward-only on the module API; freeze it "
+                                      "(requires_grad_(False)) or train with train_engine.RDTrainer")
         out4 = self._run(self._executor(), K.to_nc4(x.detach().contiguous()))
         return K.from_nc4(out4, self.out_channels)
 

@@ -1654,6 +1654,8 @@ static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStre
       if (epi == EPI_GDN_BWD) return launch_up<5, 4, EPI_GDN_BWD, FX_T>(p, st);
       if (epi == EPI_IGDN_BWD) return launch_up<5, 4, EPI_IGDN_BWD, FX_T>(p, st);
     }
+    // bmshj2018 q6-8 training (C = 192): the g_a GDN input-gradients with t = dL/dn for the parameter grads
+    if (fx == FX_T && it == 6 && epi == EPI_GDN_BWD) return launch_up<5, 6, EPI_GDN_BWD, FX_T>(p, st);
     if (fx != 0) return -4;
     if (it == 1) {
       if (epi == EPI_BIAS) return launch_up<5, 1, EPI_BIAS, 0>(p, st);

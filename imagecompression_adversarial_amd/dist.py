@@ -57,6 +57,13 @@ def allreduce_mean_(t: torch.Tensor, group=None, world: int | None = None) -> to
     return t
 
 
+def allreduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place sum over ranks (one collective for the whole buffer)."""
+    if group is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
 def couple_loss_i(loss_i: torch.Tensor, B_global: int, group=None) -> torch.Tensor:
     """Batch-coupled attack semantics: every entry of loss_i (per-image input MSEs of this rank's shard)
     becomes the mean over the global batch (attack_rd.py:333 applied to the whole batch)."""

@@ -108,9 +108,11 @@ class HyperAnalysis:
     def __init__(self, sd: dict, prefix: str = "h_a"):
         self.M = _P(sd, prefix, "0.weight").shape[1]
         self.N = _P(sd, prefix, "0.weight").shape[0]
+        # q6-8 (N = 192): the k5 s2 input-gradients (conv_up into 192 channels, the fine-tune) run 6 row tiles
+        r6 = 6 if self.N == 192 else 0
         self.convs = [K.PackedConv(_P(sd, prefix, "0.weight"), _P(sd, prefix, "0.bias"), "conv", 1),
-                      K.PackedConv(_P(sd, prefix, "2.weight"), _P(sd, prefix, "2.bias"), "conv", 2),
-                      K.PackedConv(_P(sd, prefix, "4.weight"), _P(sd, prefix, "4.bias"), "conv", 2)]
+                      K.PackedConv(_P(sd, prefix, "2.weight"), _P(sd, prefix, "2.bias"), "conv", 2, it_bwd=r6),
+                      K.PackedConv(_P(sd, prefix, "4.weight"), _P(sd, prefix, "4.bias"), "conv", 2, it_bwd=r6)]
 
     def forward(self, y4, take_abs=True):
         a = K.abs_(y4) if take_abs else y4

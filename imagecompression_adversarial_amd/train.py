@@ -61,12 +61,13 @@ class RateDistortionLoss:
             out["psnr"] = -10.0 * math.log10(float(out["mse_loss"]))
             out["msim_dB"] = -10.0 * math.log10(1.0 - float(out["msim_loss"]))
             return out
+        lamb_r = 0.0 if self.lmbda == 100 else 1.0   # train.py:77-83 "Inf Mode"
         if self.metric == "mse":
             out["distortion_loss"] = torch.mean((x_hat - target) ** 2)
-            out["loss"] = self.lmbda * 255 ** 2 * out["distortion_loss"] + bpp
+            out["loss"] = self.lmbda * 255 ** 2 * out["distortion_loss"] + lamb_r * bpp
         else:
             out["distortion_loss"] = MS.ms_ssim(x_hat, target, data_range=1.0)
-            out["loss"] = self.lmbda * (1 - out["distortion_loss"]) + bpp
+            out["loss"] = self.lmbda * (1 - out["distortion_loss"]) + lamb_r * bpp
         return out
 
 
@@ -75,9 +76,15 @@ def main_parameters(net):
 
 
 def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, group=None, world=1, qnoise=None):
-    """One outer step of train.py:335-366 on this rank's shard; grads averaged over ranks.
+    """One outer step of train.py:335-366 on this rank's shard.  The loss of the reference is a mean over the
+    GLOBAL batch, so each rank's gradient and loss values (means over its shard) are weighted by
+    B_local / B_global and summed over ranks: exact for uneven shards too (one flat all-reduce).
     qnoise: optional (noise_y, noise_z) train-mode quantisation noise for this shard (tests)."""
     batch_x = batch_x.detach().contiguous()
+    B_local = batch_x.shape[0]
+    if B_local == 0:
+        raise ValueError("empty shard: the global batch must hold at least one image per rank")
+    B_global = D.global_count(B_local, batch_x.device, group)
     for p in net.parameters():
         p.requires_grad_(False)
     res = attack_batch(net.kernels(), batch_x, steps=args.steps, epsilon=args.epsilon, noise_thr=args.noise,
@@ -92,7 +99,15 @@ def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, g
     optimizer.zero_grad(set_to_none=False)
     aux_optimizer.zero_grad()
     out = trainer.step(batch_adv, *(qnoise or ()))
-    D.allreduce_mean_(trainer.flat_grad, group, world)
+    if group is not None:
+        w = B_local / B_global
+        trainer.flat_grad.mul_(w)
+        D.allreduce_sum_(trainer.flat_grad, group)
+        keys = ("loss", "bpp_loss", "distortion_loss")
+        vals = torch.stack([torch.as_tensor(out[k], device=batch_x.device, dtype=torch.float32).reshape(())
+                            for k in keys]) * w
+        D.allreduce_sum_(vals, group)
+        out.update({k: vals[i] for i, k in enumerate(keys)})
     torch.nn.utils.clip_grad_norm_(main_parameters(net), 1.0)
     optimizer.step()
     aux_loss = net.aux_loss()
@@ -106,6 +121,9 @@ def _batches(args, rank, world, device):
     """Yield this rank's shard of each global batch (batch_size images of 256x256 crops)."""
     g = torch.Generator().manual_seed(1234)
     src = args.source
+    gb = int(src.split(":", 1)[1].split("x")[0]) if src.startswith("synthetic:") else args.batch_size
+    if gb < world:
+        raise ValueError(f"global batch {gb} < {world} ranks: every rank needs at least one image")
     if src.startswith("synthetic:"):
         B, H, W = (int(v) for v in src.split(":", 1)[1].split("x"))
         sl = D.shard_range(B, rank, world)

@@ -35,6 +35,68 @@ from . import msssim as MS
 GAMMA_BOUND = 2.0 ** -18  # NonNegativeParametrizer(minimum=0): sqrt(0 + 2^-36)
 
 
+def gdn_param_grads(raw_beta, raw_gamma, t4, saved, C, g_beta, g_gamma):
+    """GDN/IGDN parameter grads from t = dL/dn (the GDN-bwd epilogue's save_t) and the layer's saved (y, s):
+    dbeta' = sum_p t, dgamma'[c][j] = sum_p t_c x_j^2, then the NonNegativeParametrizer chain (utils/ops.py:62-89)
+    back to the raw parameters, written into g_beta / g_gamma."""
+    y4, s4 = saved
+    dbeta_e = torch.empty(C, device=t4.device)
+    K.channel_sum(t4, C, dbeta_e)
+    xsq = K.gdn_xsq(y4, s4)
+    dgamma_e = torch.empty(C * C, device=t4.device)
+    K.wgrad(t4, C, xsq, C, 1, 1, dgamma_e)
+    K.reparam_bwd(raw_beta, dbeta_e, g_beta, K.GDN_BETA_BOUND)
+    K.reparam_bwd(raw_gamma, dgamma_e, g_gamma, GAMMA_BOUND)
+
+
+def synthesis_backward(ex, g4, y_in4, saved, params, grads, prefix):
+    """g_s backward (engine.Synthesis): the input gradient (returned) and the weight / bias / IGDN parameter
+    gradients, written into grads[prefix + name] (CompressAI names: 0.weight, 1.beta, ...)."""
+    N, M = ex.N, ex.M
+    g, C = g4, 3
+    for i in (3, 2, 1, 0):
+        p = ex.convs[i]
+        cin = M if i == 0 else N
+        inp = y_in4 if i == 0 else saved[i - 1][0]
+        K.wgrad(inp, cin, g, C, 5, 2, grads[f"{prefix}{2 * i}.weight"])
+        K.channel_sum(g, C, grads[f"{prefix}{2 * i}.bias"])
+        if i > 0:
+            t = torch.empty_like(saved[i - 1][0])
+            g, _, _ = K.conv_down(g, C, p.bwd, None, N, 5, 2, K.EPI_IGDN_BWD, ex.gdns[i - 1],
+                                  saved=saved[i - 1], save_t=t, it=p.it_bwd)
+            q = f"{prefix}{2 * i - 1}"
+            gdn_param_grads(params[f"{q}.beta"], params[f"{q}.gamma"], t, saved[i - 1], N, grads[f"{q}.beta"],
+                            grads[f"{q}.gamma"])
+        else:
+            g, _, _ = K.conv_down(g, C, p.bwd, None, M, 5, 2, K.EPI_BIAS)
+        C = N
+    return g
+
+
+def analysis_backward(ex, gy4, x4, saved, params, grads, prefix, input_grad=False):
+    """g_a backward (engine.Analysis): weight / bias / GDN parameter gradients into grads[prefix + name], and
+    the input gradient (nChw4c, 3 channels) when input_grad."""
+    N, M = ex.N, ex.M
+    g, C = gy4, M
+    for i in (3, 2, 1, 0):
+        inp = x4 if i == 0 else saved[i - 1][0]
+        cin = 3 if i == 0 else N
+        K.wgrad(g, C, inp, cin, 5, 2, grads[f"{prefix}{2 * i}.weight"])
+        K.channel_sum(g, C, grads[f"{prefix}{2 * i}.bias"])
+        if i > 0:
+            t = torch.empty_like(saved[i - 1][0])
+            g, _, _ = K.conv_up(g, C, ex.convs[i].bwd, None, N, K.EPI_GDN_BWD, ex.gdns[i - 1],
+                                saved=saved[i - 1], save_t=t, it=ex.convs[i].it_bwd)
+            q = f"{prefix}{2 * i - 1}"
+            gdn_param_grads(params[f"{q}.beta"], params[f"{q}.gamma"], t, saved[i - 1], N, grads[f"{q}.beta"],
+                            grads[f"{q}.gamma"])
+        C = N
+    if input_grad:
+        gx, _, _ = K.conv_up(g, N, ex.convs[0].bwd, None, 3, K.EPI_BIAS, prec=ex.convs[0].bwd_prec)
+        return gx
+    return None
+
+
 class RDTrainer:
     """HIP train step for a ``codec.FactorizedPrior`` / ``codec.ScaleHyperprior``."""
 
@@ -43,9 +105,10 @@ class RDTrainer:
             raise ValueError(f"metric {metric!r}: the HIP trainer supports mse and ms-ssim (lpips is out of scope)")
         self.net, self.metric, self.lmbda = net, metric, float(lmbda)
         self.kind = net.model_kind
-        if net.g_a[0].weight.shape[0] != 128:
-            raise NotImplementedError("the HIP train step covers N = 128 (quality 1-5); q6-8 (N = 192) runs the "
-                                      "attack / eval paths only")
+        # train.py:77-83: lambda == 100 is the reference's "Inf mode", the rate term leaves the loss (lamb_r = 0)
+        self.lamb_r = 0.0 if self.lmbda == 100 else 1.0
+        if self.lamb_r == 0.0:
+            print("[WARNING] Inf Mode")
         named = dict(net.named_parameters())
         self.names = sorted(n for n in named if not n.endswith(".quantiles"))
         self.params = {n: named[n] for n in self.names}
@@ -69,52 +132,13 @@ class RDTrainer:
         return self.views[name]
 
     # ------------------------------------------------------------------ #
-    def _gdn_param_grads(self, prefix, t4, saved, C):
-        """GDN/IGDN parameter grads from t = dL/dn and the saved (y, s) of that layer."""
-        y4, s4 = saved
-        dbeta_e = torch.empty(C, device=t4.device)
-        K.channel_sum(t4, C, dbeta_e)
-        xsq = K.gdn_xsq(y4, s4)
-        dgamma_e = torch.empty(C * C, device=t4.device)
-        K.wgrad(t4, C, xsq, C, 1, 1, dgamma_e)
-        K.reparam_bwd(self.params[f"{prefix}.beta"], dbeta_e, self._g(f"{prefix}.beta"), K.GDN_BETA_BOUND)
-        K.reparam_bwd(self.params[f"{prefix}.gamma"], dgamma_e, self._g(f"{prefix}.gamma"), GAMMA_BOUND)
-
     def _g_s_backward(self, ex, g4, y_in4, saved):
         """Synthesis backward with weight / bias / IGDN grads; returns dL/d(g_s input)."""
-        N, M = ex.N, ex.M
-        g, C = g4, 3
-        for i in (3, 2, 1, 0):
-            p = ex.convs[i]
-            cin = M if i == 0 else N
-            inp = y_in4 if i == 0 else saved[i - 1][0]
-            K.wgrad(inp, cin, g, C, 5, 2, self._g(f"g_s.{2 * i}.weight"))
-            K.channel_sum(g, C, self._g(f"g_s.{2 * i}.bias"))
-            if i > 0:
-                t = torch.empty_like(saved[i - 1][0])
-                g, _, _ = K.conv_down(g, C, p.bwd, None, N, 5, 2, K.EPI_IGDN_BWD, ex.gdns[i - 1],
-                                      saved=saved[i - 1], save_t=t)
-                self._gdn_param_grads(f"g_s.{2 * i - 1}", t, saved[i - 1], N)
-            else:
-                g, _, _ = K.conv_down(g, C, p.bwd, None, M, 5, 2, K.EPI_BIAS)
-            C = N
-        return g
+        return synthesis_backward(ex, g4, y_in4, saved, self.params, self.views, "g_s.")
 
     def _g_a_backward(self, ex, gy4, x4, saved):
         """Analysis backward with weight / bias / GDN grads (no input gradient)."""
-        N, M = ex.N, ex.M
-        g, C = gy4, M
-        for i in (3, 2, 1, 0):
-            inp = x4 if i == 0 else saved[i - 1][0]
-            cin = 3 if i == 0 else N
-            K.wgrad(g, C, inp, cin, 5, 2, self._g(f"g_a.{2 * i}.weight"))
-            K.channel_sum(g, C, self._g(f"g_a.{2 * i}.bias"))
-            if i > 0:
-                t = torch.empty_like(saved[i - 1][0])
-                g, _, _ = K.conv_up(g, C, ex.convs[i].bwd, None, N, K.EPI_GDN_BWD, ex.gdns[i - 1],
-                                    saved=saved[i - 1], save_t=t)
-                self._gdn_param_grads(f"g_a.{2 * i - 1}", t, saved[i - 1], N)
-            C = N
+        analysis_backward(ex, gy4, x4, saved, self.params, self.views, "g_a.")
 
     def _eb_backward(self, ck, v4, lik4, C, scale):
         gl = K.bpp_grad(lik4, scale)
@@ -137,6 +161,7 @@ class RDTrainer:
         x4 = K.to_nc4(x)
         npx = B * H * W
         bscale = 1.0 / (-math.log(2) * npx)
+        gscale = bscale * self.lamb_r   # d loss / d log-likelihood (0 in Inf mode)
 
         y4, sa = ck.ga.forward(x4, save=True)
         yshape = (B, M, H // 16, W // 16)
@@ -155,8 +180,8 @@ class RDTrainer:
             if noise_z is None:
                 noise_z = torch.empty((B, N, H // 64, W // 64), device=x.device).uniform_(-0.5, 0.5)
             zt4, zlik4, _ = K.eb_likelihood(z4, N, ck.eb, True, K.to_nc4(noise_z.contiguous()))
-            s1, _, _ = K.conv_up(zt4, N, hs.convs[0].fwd, hs.convs[0].bias, N, K.EPI_RELU)
-            s2, _, _ = K.conv_up(s1, N, hs.convs[1].fwd, hs.convs[1].bias, N, K.EPI_RELU)
+            s1, _, _ = K.conv_up(zt4, N, hs.convs[0].fwd, hs.convs[0].bias, N, K.EPI_RELU, it=hs.convs[0].it_fwd)
+            s2, _, _ = K.conv_up(s1, N, hs.convs[1].fwd, hs.convs[1].bias, N, K.EPI_RELU, it=hs.convs[1].it_fwd)
             sig4, _, _ = K.conv_down(s2, N, hs.convs[2].fwd, hs.convs[2].bias, M, 3, 1, K.EPI_RELU)
             yt4, ylik4, _ = K.gc_likelihood(y4, M, sig4, None, True, ny4)
             liks = [ylik4, zlik4]
@@ -168,23 +193,23 @@ class RDTrainer:
         if self.metric == "mse":
             dist = K.sqdiff_mean(K.from_nc4(xh4, 3), x).mean()
             K.mse_grad_(xh4, x, g4, self.lmbda * 255.0 ** 2 * 2.0 / (B * 3 * H * W))
-            loss = self.lmbda * 255.0 ** 2 * dist + bpp
+            loss = self.lmbda * 255.0 ** 2 * dist + self.lamb_r * bpp
         else:
             xh = K.from_nc4(xh4, 3)
             v, gX, _ = MS.ms_ssim_value_and_grad(xh, x, torch.full((B,), -self.lmbda / B, device=x.device),
                                                  data_range=1.0, mode=0)
             dist = v.mean()
             g4 = K.to_nc4(gX)
-            loss = self.lmbda * (1.0 - dist) + bpp
+            loss = self.lmbda * (1.0 - dist) + self.lamb_r * bpp
 
         # ---- backward ----
         gyt = self._g_s_backward(ck.gs, g4, yt4, ss)
         del ss, g4
         if self.kind == "factorized":
-            gv = self._eb_backward(ck, yt4, ylik4, M, bscale)
+            gv = self._eb_backward(ck, yt4, ylik4, M, gscale)
             gy = gyt.add_(gv)
         else:
-            gl_y = K.bpp_grad(ylik4, bscale)
+            gl_y = K.bpp_grad(ylik4, gscale)
             gy_gc, gsig = K.gc_bwd(yt4, sig4, gl_y, M)
             gy = gyt.add_(gy_gc)
             # h_s backward
@@ -201,15 +226,15 @@ class RDTrainer:
             K.channel_sum(g, N, self._g("h_s.0.bias"))
             gz, _, _ = K.conv_down(g, N, hs.convs[0].bwd, None, N, 5, 2, K.EPI_BIAS)
             # EntropyBottleneck backward (z_tilde = z + u)
-            gz.add_(self._eb_backward(ck, zt4, zlik4, N, bscale))
+            gz.add_(self._eb_backward(ck, zt4, zlik4, N, gscale))
             # h_a backward
             K.wgrad(gz, N, z2, N, 5, 2, self._g("h_a.4.weight"))
             K.channel_sum(gz, N, self._g("h_a.4.bias"))
-            g, _, _ = K.conv_up(gz, N, ha.convs[2].bwd, None, N, K.EPI_BIAS)
+            g, _, _ = K.conv_up(gz, N, ha.convs[2].bwd, None, N, K.EPI_BIAS, it=ha.convs[2].it_bwd)
             K.relu_bwd_(g, z2)
             K.wgrad(g, N, z1, N, 5, 2, self._g("h_a.2.weight"))
             K.channel_sum(g, N, self._g("h_a.2.bias"))
-            g, _, _ = K.conv_up(g, N, ha.convs[1].bwd, None, N, K.EPI_BIAS)
+            g, _, _ = K.conv_up(g, N, ha.convs[1].bwd, None, N, K.EPI_BIAS, it=ha.convs[1].it_bwd)
             K.relu_bwd_(g, z1)
             K.wgrad(g, N, a4, M, 3, 1, self._g("h_a.0.weight"))
             K.channel_sum(g, N, self._g("h_a.0.bias"))

@@ -245,19 +245,53 @@ def ifgsm(P, im_s, steps=10, epsilon=16.0, momentum=False, model="hyper"):
 
 
 def rd_loss(out, target, metric="mse", lmbda=0.0067):
-    """train.RateDistortionLoss.forward(training=True) (train.py:52-96)."""
+    """train.RateDistortionLoss.forward(training=True) (train.py:52-96), incl. the "Inf Mode" of
+    lmbda == 100 (train.py:77-83: the rate term leaves the loss)."""
     N, _, H, W = target.shape
     num_pixels = N * H * W
     bpp = 0.0
     for lik in out["likelihoods"].values():
         lik = torch.clamp(lik, min=1.0 / 65536)
         bpp = bpp + torch.log(lik).sum() / (-math.log(2) * num_pixels)
+    lamb_r = 0.0 if lmbda == 100 else 1.0
     if metric == "mse":
         d = torch.mean((out["x_hat"] - target) ** 2)
-        loss = lmbda * 255 ** 2 * d + bpp
+        loss = lmbda * 255 ** 2 * d + lamb_r * bpp
     elif metric == "ms-ssim":
         d = ms_ssim(out["x_hat"], target, data_range=1.0)
-        loss = lmbda * (1 - d) + bpp
+        loss = lmbda * (1 - d) + lamb_r * bpp
     else:
         raise ValueError(metric)
     return {"loss": loss, "bpp_loss": bpp, "distortion_loss": d}
+
+
+def adv_train_step(P, batch_x, steps=300, noise_thr=1e-4, epsilon=16.0, lr_attack=0.01, att_metric="L2",
+                   clamp=True, model="hyper", metric="mse", lmbda=0.0130, lr_train=1e-4, noise_y=None,
+                   noise_z=None):
+    """One outer step of train.py --adv (train.py:335-366): the batch-coupled inner attack (attack_rd.attack_
+    on the whole batch, train.py:342), the train-mode forward of the adversarial batch with the given
+    quantisation noise, RateDistortionLoss against that same batch (:349-351), backward,
+    clip_grad_norm_(1.0) over the main parameters (:360), Adam(lr_train) (:361), then the aux loss of the
+    EntropyBottleneck quantiles and its Adam(1e-3) (:363-366; coder.py:50-86 optimiser split).
+    Returns (updated params dict, loss values, aux loss, the adversarial batch)."""
+    r = attack(P, batch_x, steps=steps, epsilon=epsilon, noise_thr=noise_thr, lr=lr_attack, att_metric=att_metric,
+               clamp=clamp, model=model, coupled=True, eval_msssim=False)
+    batch_adv = r.im_adv.detach()
+    main_names = sorted(k for k in P if not k.endswith(".quantiles"))
+    aux_names = sorted(k for k in P if k.endswith(".quantiles"))
+    Q = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
+    opt = torch.optim.Adam([Q[k] for k in main_names], lr=lr_train)
+    aux_opt = torch.optim.Adam([Q[k] for k in aux_names], lr=1e-3)
+    res = codec.forward(Q, batch_adv, model, training=True, noise_y=noise_y, noise_z=noise_z)
+    out = rd_loss(res, batch_adv, metric, lmbda)
+    opt.zero_grad()
+    aux_opt.zero_grad()
+    out["loss"].backward()
+    torch.nn.utils.clip_grad_norm_([Q[k] for k in main_names], 1.0)
+    opt.step()
+    aux_loss = codec.eb_aux_loss(Q)
+    aux_opt.zero_grad()
+    aux_loss.backward()
+    aux_opt.step()
+    return ({k: v.detach() for k, v in Q.items()}, {k: float(v) for k, v in out.items()}, float(aux_loss),
+            batch_adv)

@@ -13,7 +13,8 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-B, H, W = 4, 128, 128
+H, W = 128, 128
+B = 4
 
 
 def _free_port():
@@ -22,7 +23,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _inputs():
+def _inputs(B=4):
     g = torch.Generator().manual_seed(7)
     x = torch.rand((B, 3, H, W), generator=g)
     ny = torch.rand((B, 192, H // 16, W // 16), generator=g) - 0.5
@@ -35,7 +36,7 @@ def _args():
                            round_adv=False)
 
 
-def _one_step(rank, world, group):
+def _one_step(rank, world, group, B=4):
     from imagecompression_adversarial_amd import codec, coder
     from imagecompression_adversarial_amd.train import adv_step
     from imagecompression_adversarial_amd.train_engine import RDTrainer
@@ -45,7 +46,7 @@ def _one_step(rank, world, group):
     net = net.to("cuda:0").train()
     opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=1e-4))
     tr = RDTrainer(net, "mse", 0.0130)
-    x, ny, nz = _inputs()
+    x, ny, nz = _inputs(B)
     sl = D.shard_range(B, rank, world)
     sh = slice(sl.start, sl.stop)
     out, _ = adv_step(net, tr, opt, aux, x[sh].cuda(), _args(), group, world,
@@ -55,7 +56,7 @@ def _one_step(rank, world, group):
     return flat, float(out["loss"])
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, B=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
@@ -63,7 +64,7 @@ def _worker(rank, world, port, q):
         from imagecompression_adversarial_amd import dist as D
         torch.cuda.set_device(0)
         r, w, group = D.init_from_env("gloo")
-        flat, loss = _one_step(r, w, group)
+        flat, loss = _one_step(r, w, group, B)
         q.put((rank, flat, loss, None))
     except Exception as e:  # surface failures to the parent
         q.put((rank, None, None, repr(e)))
@@ -72,12 +73,15 @@ def _worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def test_dp_adv_step_matches_single_process():
-    ref_flat, ref_loss = _one_step(0, 1, None)
+@pytest.mark.parametrize("world,nb", [(2, 4), (3, 5)])
+def test_dp_adv_step_matches_single_process(world, nb):
+    """(3, 5): uneven shards 1/2/2: every rank's gradient and loss are weighted by its share of
+    the global batch, so the step still equals the whole-batch step."""
+    ref_flat, ref_loss = _one_step(0, 1, None, nb)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, nb)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -87,13 +91,15 @@ def test_dp_adv_step_matches_single_process():
         res[rank] = (flat, loss)
     for p in procs:
         p.join(timeout=60)
-    assert torch.equal(res[0][0], res[1][0]), "replicas diverged"
+    for r in range(1, world):
+        assert torch.equal(res[0][0], res[r][0]), "replicas diverged"
     d = (res[0][0] - ref_flat).abs().max().item()
     moved = (ref_flat - _init_flat()).abs().max().item()
     assert moved > 0
     assert d <= 2e-3 * moved, (d, moved)
-    # each rank reports its shard's loss; the whole-batch loss is their mean
-    assert abs(0.5 * (res[0][1] + res[1][1]) - ref_loss) <= 1e-3 * abs(ref_loss)
+    # every rank reports the whole-batch loss (shard means weighted by shard size, summed)
+    for r in range(world):
+        assert abs(res[r][1] - ref_loss) <= 1e-3 * abs(ref_loss)
 
 
 def _init_flat():

@@ -18,9 +18,9 @@ def rnd(shape, seed, lo=0.0, hi=1.0):
     return torch.rand(shape, generator=g) * (hi - lo) + lo
 
 
-def _net(model, P):
+def _net(model, P, quality=3):
     from imagecompression_adversarial_amd import codec
-    net = codec.bmshj2018_hyperprior(3) if model == "hyper" else codec.bmshj2018_factorized(3)
+    net = codec.bmshj2018_hyperprior(quality) if model == "hyper" else codec.bmshj2018_factorized(quality)
     sd = net.state_dict()
     sd.update({k: v.reshape(sd[k].shape) for k, v in P.items() if k in sd})
     net.load_state_dict(sd)
@@ -35,18 +35,23 @@ def _oracle_grads(P, x, model, metric, lmbda, ny, nz):
     return out, {k: v.grad for k, v in Pr.items() if v.grad is not None}
 
 
-@pytest.mark.parametrize("model,metric,H,W", [("hyper", "mse", 128, 128), ("hyper", "ms-ssim", 192, 192),
-                                              ("factorized", "mse", 128, 192)])
-def test_rd_backward_vs_oracle(model, metric, H, W):
+@pytest.mark.parametrize("model,metric,H,W,q,lmbda", [
+    ("hyper", "mse", 128, 128, 3, None), ("hyper", "ms-ssim", 192, 192, 3, None), ("factorized", "mse", 128, 192, 3, None),
+    # quality 6-8 (N = 192, M = 320): the C = 192 GDN layers train on the 6-row-tile kernels
+    ("hyper", "mse", 128, 128, 6, None), ("factorized", "ms-ssim", 192, 192, 7, None),
+    # lambda == 100: the reference's "Inf Mode", rate term out of the loss (train.py:77-83)
+    ("hyper", "mse", 128, 128, 3, 100.0)])
+def test_rd_backward_vs_oracle(model, metric, H, W, q, lmbda):
     from imagecompression_adversarial_amd.train_engine import RDTrainer
-    P = oc.perturb_params(oc.init_params(model, 3, seed=0), seed=1)
+    P = oc.perturb_params(oc.init_params(model, q, seed=0), seed=1)
     B = 2
     x = rnd((B, 3, H, W), 5)
-    N, M = 128, 192
+    N, M = oc.model_channels(model, q)
     ny = rnd((B, M, H // 16, W // 16), 6, -0.5, 0.5)
     nz = rnd((B, N, H // 64, W // 64), 7, -0.5, 0.5) if model == "hyper" else None
-    lmbda = 0.0130 if metric == "mse" else 8.73
-    net = _net(model, P)
+    if lmbda is None:
+        lmbda = 0.0130 if metric == "mse" else 8.73
+    net = _net(model, P, q)
     tr = RDTrainer(net, metric, lmbda)
     got = tr.step(x.to(DEV), ny.to(DEV), None if nz is None else nz.to(DEV))
     torch.cuda.synchronize()
@@ -90,3 +95,43 @@ def test_rd_backward_batch_sum_property():
     torch.cuda.synchronize()
     assert rel_err(((a + b) / 2).cpu(), full.cpu()) < 1e-3
     assert torch.isfinite(full).all()
+
+
+def test_adv_train_step_vs_oracle():
+    """One whole outer step of train.py --adv (train.py:335-366) vs oracle.attack.adv_train_step: the
+    batch-coupled inner attack, the train-mode RD backward, clip_grad_norm_(1.0), Adam and the aux Adam.
+    The first Adam step moves a parameter by ~lr * g / (|g| + eps), so parameters whose gradient is near 0
+    or changes sign under fp32 reordering may move differently: bounded by the 99.9th percentile of the
+    difference (<= 1e-2 of the step size) and the max (<= 2 steps)."""
+    from types import SimpleNamespace
+    from imagecompression_adversarial_amd import coder
+    from imagecompression_adversarial_amd.train import adv_step
+    from imagecompression_adversarial_amd.train_engine import RDTrainer
+    P = oc.perturb_params(oc.init_params("hyper", 3, seed=0), seed=1)
+    B, H, W = 3, 128, 128
+    x = rnd((B, 3, H, W), 41)
+    ny = rnd((B, 192, H // 16, W // 16), 42, -0.5, 0.5)
+    nz = rnd((B, 128, H // 64, W // 64), 43, -0.5, 0.5)
+    lr_train, lmbda = 1e-4, 0.0130
+    net = _net("hyper", P)
+    opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=lr_train))
+    tr = RDTrainer(net, "mse", lmbda)
+    args = SimpleNamespace(steps=4, epsilon=16.0, noise=1e-4, lr_attack=0.01, att_metric="L2", clamp=True,
+                           round_adv=False)
+    out, batch_adv = adv_step(net, tr, opt, aux, x.to(DEV), args, qnoise=(ny.to(DEV), nz.to(DEV)))
+    torch.cuda.synchronize()
+    Pn, ref_out, ref_aux, ref_adv = oa.adv_train_step(P, x, steps=4, lmbda=lmbda, lr_train=lr_train,
+                                                       noise_y=ny, noise_z=nz)
+    assert rel_err(batch_adv.cpu(), ref_adv) < 1e-5
+    for k in ("loss", "bpp_loss", "distortion_loss"):
+        assert abs(float(out[k]) - ref_out[k]) <= 1e-4 * max(abs(ref_out[k]), 1.0), k
+    assert abs(float(out["aux_loss"]) - ref_aux) <= 1e-4 * max(abs(ref_aux), 1.0)
+    named = dict(net.named_parameters())
+    worst = []
+    for k, v in Pn.items():
+        step = lr_train if not k.endswith(".quantiles") else 1e-3
+        d = (named[k].detach().cpu().reshape(v.shape) - v).abs() / step
+        worst.append((float(d.max()), float(torch.quantile(d.flatten().double(), 0.999)) if d.numel() > 1 else 0.0, k))
+    worst.sort(reverse=True)
+    assert worst[0][0] <= 2.0, worst[:3]
+    assert max(w[1] for w in worst) <= 1e-2, sorted(worst, key=lambda w: -w[1])[:3]
