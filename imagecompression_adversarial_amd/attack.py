@@ -78,6 +78,20 @@ def eval_forward(kern: CodecKernels, x: torch.Tensor, clamp=True):
     return out, K.bits_to_bpp(res["sumlog"], H * W)
 
 
+def padded_eval_forward(kern: CodecKernels, x: torch.Tensor, pad: int, mode="reflect", clamp=True):
+    """attack_rd.py:389-419 with -p: net(F.pad(x, (p, p, p, p), mode)) -> crop(x_hat), bits / (H * W)."""
+    import torch.nn.functional as F
+    B, _, H, W = x.shape
+    xp = F.pad(x, (pad, pad, pad, pad), mode=mode).contiguous()
+    Hp, Wp = xp.shape[2:]
+    if Hp % 64 or Wp % 64:
+        raise ValueError(f"-p {pad}: the padded size {Hp}x{Wp} must be a multiple of 64 (the codec's latent grid; "
+                         "the reference's crop fails otherwise)")
+    out_p, bpp_p = eval_forward(kern, xp, clamp)
+    out = out_p[:, :, pad:pad + H, pad:pad + W].contiguous()
+    return out, bpp_p * (Hp * Wp / (H * W))
+
+
 def evaluate(kern, im_in, im_s, output_s, clamp=True, adv=False, msssim=True):
     """self_ensemble.eval (self_ensemble.py:173-252), per image."""
     im_ = K.clamp01(im_in) if clamp else im_in
@@ -108,7 +122,7 @@ class AttackLoop:
 
     def __init__(self, kern: CodecKernels, im_s: torch.Tensor, steps=1001, epsilon=16.0, noise_thr=1e-4,
                  lr=0.01, att_metric="L2", clamp=True, init_noise=None, coupled=False, group=None,
-                 target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0):
+                 target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0, pad=None, padding_mode="reflect"):
         if att_metric not in ("L2", "ms-ssim"):
             raise ValueError(f"att_metric {att_metric!r} not supported (reference: L2, ms-ssim)")
         if target is not None and (att_metric != "L2" or coupled):
@@ -148,7 +162,13 @@ class AttackLoop:
         self.census = torch.zeros(B, dtype=torch.int32, device=dev)
         self.steps_done = 0
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
-        self.output_s, self.bpp_ori = eval_forward(kern, self.im_s, clamp)
+        if pad:
+            # -p P (attack_rd.py:389-413): the pre-eval codes the image padded by P (-padmode, reflect by default),
+            # output_s is the crop back to the image, bpp_ori counts the padded bits per UNPADDED pixel (:419);
+            # the step loop and the post-eval run unpadded, as in the reference
+            self.output_s, self.bpp_ori = padded_eval_forward(kern, self.im_s, int(pad), padding_mode, clamp)
+        else:
+            self.output_s, self.bpp_ori = eval_forward(kern, self.im_s, clamp)
         self.output_s4 = None
         self.roi = None
         if target is not None:
@@ -302,9 +322,10 @@ def roi_mse(a, b, roi4):
 
 def attack_batch(kern: CodecKernels, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
                  clamp=True, init_noise=None, eval_msssim=True, record=False, coupled=False,
-                 group=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0) -> AttackResult:
+                 group=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0, pad=None,
+                 padding_mode="reflect") -> AttackResult:
     loop = AttackLoop(kern, im_s, steps, epsilon, noise_thr, lr, att_metric, clamp, init_noise, coupled, group,
-                      target, roi, la_tar, la_bkg_in, la_bkg_out)
+                      target, roi, la_tar, la_bkg_in, la_bkg_out, pad, padding_mode)
     branches = loop.run(record=record)
     im_, out, bpp, mse_in, mse_out, msim_in, msim_out, vi, vi_msim = evaluate(
         kern, loop.im_in, loop.im_s, loop.output_s, clamp, adv=False, msssim=eval_msssim)
@@ -317,14 +338,16 @@ def attack_batch(kern: CodecKernels, im_s, steps=1001, epsilon=16.0, noise_thr=1
     return res
 
 
-def ifgsm_batch(kern: CodecKernels, im_s, steps=10, epsilon=16.0, momentum=False, clamp=True):
-    """attack_ifgsm.attack_ifgsm (no random start); returns (im_adv, output_s)."""
+def ifgsm_batch(kern: CodecKernels, im_s, steps=10, epsilon=16.0, momentum=False, clamp=True, x0=None):
+    """The step loop of attack_ifgsm.attack_ifgsm (attack_ifgsm.py:392-423) per image; x0: the start point
+    (the random start clamp(im_s + U(-eps, eps), 0, 1) of :377-380; default im_s, :382).
+    Returns (im_adv, output_s)."""
     B, _, H, W = im_s.shape
     im_s = im_s.contiguous()
     output_s, _ = eval_forward(kern, im_s, clamp=True)
     eps = float(epsilon) / 255.0
     alpha = float(eps / steps)
-    x = im_s.clone()
+    x = im_s.clone() if x0 is None else x0.contiguous().clone()
     gacc = torch.zeros_like(x)
     part = torch.empty(B * K.blocks_per_image(), device=x.device)
     grad4 = K.empty_nc4(B, 3, H, W, x.device)

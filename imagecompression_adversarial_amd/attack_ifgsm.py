@@ -1,6 +1,6 @@
 """Drop-in for attack_ifgsm.py: I-FGSM / MI-FGSM (grad-sign + L-inf projection) on HIP.
 
-attack_ifgsm   attack_ifgsm.py:364-438 (random_start=False, multi_start=1 path)
+attack_ifgsm   attack_ifgsm.py:364-438 (incl. random_start / multi_start)
 mifgsm_attack  attack_ifgsm.py:348-362  (fused into ica_ifgsm_step)
 eval           attack_ifgsm.py:216-273  (no MS-SSIM)
 
@@ -17,15 +17,38 @@ from .attack import evaluate, ifgsm_batch
 from .attack_rd import _sources
 
 
-def attack_ifgsm(im_s, net, args, random_start=False, multi_start=1, momentum=False):
-    """Returns (im_adv, output_adv, output_s, bpp_ori, bpp, mse_in, mse_out, vi) per batch (lists for vi)."""
-    if random_start or multi_start > 1:
-        raise NotImplementedError("random start (PGD) variant is not on the HIP path yet")
+def attack_ifgsm(im_s, net, args, random_start=False, multi_start=1, momentum=False, start_noise=None):
+    """attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438), per image.  random_start: PGD start
+    clamp(im_s + U(-eps, eps), 0, 1) (:377-380); multi_start R > 1 implies it and keeps, per image, the restart
+    with the largest vi (:434-437; a vi of None ranks lowest).  start_noise(r, shape) may supply restart r's
+    U(-eps, eps) draw (default: the device generator).
+    Returns (im_adv, output_adv, output_s, bpp_ori, bpp, mse_in, mse_out, vi) per batch (lists for vi)."""
     kern = net.kernels()
     from .attack import eval_forward
     _, bpp_ori = eval_forward(kern, im_s, clamp=True)
-    x, output_s = ifgsm_batch(kern, im_s, steps=args.steps, epsilon=args.epsilon, momentum=momentum)
-    im_, out, bpp, mse_in, mse_out, _, _, vi, _ = evaluate(kern, x, im_s, output_s, clamp=args.clamp, msssim=False)
+    eps = args.epsilon / 255.0
+    if multi_start > 1:
+        random_start = True
+    B = im_s.shape[0]
+    best = None
+    for r in range(max(int(multi_start), 1)):
+        x0 = None
+        if random_start:
+            u = start_noise(r, im_s.shape) if start_noise is not None else torch.empty_like(im_s).uniform_(-eps, eps)
+            x0 = torch.clamp(im_s + u.to(im_s.device, im_s.dtype), 0.0, 1.0)
+        x, output_s = ifgsm_batch(kern, im_s, steps=args.steps, epsilon=args.epsilon, momentum=momentum, x0=x0)
+        im_, out, bpp, mse_in, mse_out, _, _, vi, _ = evaluate(kern, x, im_s, output_s, clamp=args.clamp,
+                                                              msssim=False)
+        if best is None:
+            best = [im_, out, bpp, mse_in, mse_out, list(vi)]
+            continue
+        key = (lambda v: -float("inf") if v is None else v)
+        for b in range(B):
+            if key(vi[b]) > key(best[5][b]):
+                for t, src in zip(best[:5], (im_, out, bpp, mse_in, mse_out)):
+                    t[b] = src[b]
+                best[5][b] = vi[b]
+    im_, out, bpp, mse_in, mse_out, vi = best
     return im_, out, output_s, bpp_ori, bpp, mse_in, mse_out, vi
 
 

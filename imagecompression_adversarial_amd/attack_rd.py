@@ -16,8 +16,9 @@ Differences from the reference, all deliberate and documented:
     prints the per-image lines in reference order and the AVG line.
   * A ``vi`` of None (mse_out == 0, reference warning at self_ensemble.py:244)
     does not crash the random-restart selection (reference compares None > float).
-  * ``-p/--pad`` and ``--defend`` are not supported (``--defend`` crashes inside the
-    reference step loop).
+  * ``--defend`` is not supported (it crashes inside the reference step loop).
+  * ``-p P`` pads only the pre-eval, as the reference does (attack_rd.py:389-419); a padded size that is not a
+    multiple of 64 raises (the reference's crop would fail on the mismatched reconstruction).
   * ``-t TARGET [--mask_loc x0 x1 y0 y1 -la_tar -la_bkg_in -la_bkg_out]`` runs the targeted / ROI attack
     the README advertises but attack_rd.py never implemented; its loss is defined in
     DESIGN.md ("Targeted / ROI attack").
@@ -48,8 +49,6 @@ def _mse_vi(res, b):
 def attack_(im_s, net, args):
     """attack_rd.attack_ for a batch: returns (im_adv, output_adv, output_s, bpp_ori, bpp, mse_results, vi_results).
     For B > 1 the metric dicts hold lists (one entry per image)."""
-    if args.pad:
-        raise NotImplementedError("-p/--pad (reflect padding) is not supported on the HIP path")
     if getattr(args, "defend", False):
         raise NotImplementedError("--defend is not supported (it crashes inside the reference step loop)")
     kern = net.kernels(getattr(args, "precision", "fp32"))
@@ -62,7 +61,7 @@ def attack_(im_s, net, args):
                    la_tar=args.lamb_tar, la_bkg_in=args.lamb_bkg_in, la_bkg_out=args.lamb_bkg_out)
     res = attack_batch(kern, im_s, steps=args.steps, epsilon=args.epsilon, noise_thr=args.noise, lr=args.lr_attack,
                        att_metric=args.att_metric, clamp=args.clamp, init_noise=init_noise,
-                       eval_msssim=min(im_s.shape[2:]) > 160, **tkw)
+                       eval_msssim=min(im_s.shape[2:]) > 160, pad=args.pad, padding_mode=args.padding_mode, **tkw)
     if im_s.shape[0] == 1:
         mse, vi = _mse_vi(res, 0)
         return res.im_adv, res.output_adv, res.output_s, res.bpp_ori[0], res.bpp[0], mse, vi

@@ -83,7 +83,16 @@ def load_model(args, training):
     if args.checkpoint:
         print("[CKPT] Loading", args.checkpoint)
         checkpoint = torch.load(args.checkpoint, map_location=args.device, weights_only=True)
-        net.load_state_dict(checkpoint["state_dict"] if "state_dict" in checkpoint else checkpoint)
+        if checkpoint.get("state_dict"):
+            net.load_state_dict(checkpoint["state_dict"])
+        else:
+            # old version ckpts (coder.py:107-116): an anchors.balle.Image_coder state dict ("net."-prefixed
+            # CompressAI names, CDF buffers of checkpoint-dependent size); converted and re-saved as
+            # {"state_dict": ...} next to it (args.checkpoint + "new"), then loaded from there
+            old = convert_old_checkpoint(checkpoint)
+            torch.save({"state_dict": old}, args.checkpoint + "new")
+            checkpoint = torch.load(args.checkpoint + "new", map_location=args.device, weights_only=True)
+            net.load_state_dict(checkpoint["state_dict"])
     print("=========================================================")
     if training:
         last_epoch = 0
@@ -95,7 +104,25 @@ def load_model(args, training):
             aux_optimizer.load_state_dict(checkpoint["aux_optimizer"])
             lr_scheduler.load_state_dict(checkpoint["lr_scheduler"])
         return net.train(), last_epoch, optimizer, aux_optimizer, lr_scheduler
+    if checkpoint is not None and getattr(args, "eval", False):
+        # evaluation of a training checkpoint (coder.py:138-146): report its epoch / step / learning rate
+        last_epoch = checkpoint["epoch"]
+        print("Trained epoch", last_epoch)
+        if checkpoint.get("step"):
+            print("Trained step", checkpoint["step"])
+        optimizer, aux_optimizer = configure_optimizers(net, args)
+        optimizer.load_state_dict(checkpoint["optimizer"])
+        print(f"Learning rate: {optimizer.param_groups[0]['lr']}")
     return net.eval()
+
+
+def convert_old_checkpoint(state_dict, prefix="net."):
+    """anchors.balle.Image_coder.load_state_dict (anchors/balle.py:57-72) + net_old.net.state_dict()
+    (coder.py:110-113): strip the wrapper's "net." prefix; the CDF buffers keep their checkpoint sizes (the
+    model's load_state_dict resizes them, anchors/utils.py:74-109)."""
+    if not state_dict or not all(k.startswith(prefix) for k in state_dict):
+        raise KeyError(f"not an old-format (Image_coder) checkpoint: keys must start with {prefix!r}")
+    return {k[len(prefix):]: v for k, v in state_dict.items()}
 
 
 def _synthetic_init(net, seed=0):

@@ -113,12 +113,10 @@ ICA_DEV void xcd_block(int& bx, int& by) {
   const unsigned nx = gridDim.x, total = nx * gridDim.y;
   const unsigned lin = blockIdx.y * nx + blockIdx.x;
   unsigned L = lin;
-#ifndef ICA_NO_XCD_REMAP
   if constexpr (REMAP) {
     const unsigned q = total >> 3, r = total & 7, x = lin & 7;
     L = x * q + (x < r ? x : r) + (lin >> 3);
   }
-#endif
   bx = (int)(L % nx);
   by = (int)(L / nx);
 }

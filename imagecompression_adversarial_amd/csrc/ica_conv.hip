@@ -479,27 +479,12 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
   }
 }
 
-// bf16 weight-fragment load of tile it at step g (timing-only ICA_ABLATE_WLOAD build: no weight traffic,
-// synthetic small values, wrong results)
-#ifdef ICA_ABLATE_WLOAD
-#define ICA_WLOAD_BF(w, it, g) \
-  __builtin_bit_cast(bf16x8, (u32x4_t){0x3c003c00u + (unsigned)(((g) + (it)) & 7), 0x3c003c00u, 0x3c003c00u, \
-                                       0x3c003c00u + (unsigned)(threadIdx.x & 3)})
-#else
+// bf16 weight-fragment load of tile it at step g
 #define ICA_WLOAD_BF(w, it, g) ((w)[(it) * 64])
-#endif
 
 // Load one (chunk, tap) weight fragment set: IT tiles x KH floats per lane.
 template <int IT, int KH>
 ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
-#ifdef ICA_ABLATE_WLOAD
-  // timing-only build: no weight traffic (wrong results)
-#pragma unroll
-  for (int it = 0; it < IT; ++it)
-#pragma unroll
-    for (int e = 0; e < KH; ++e) a[it][e] = __builtin_bit_cast(float, (int)((threadIdx.x + it * 7 + e + (int)(size_t)w) & 0x3f) | 0x3c000000);
-  return;
-#endif
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     if constexpr (KH == 8) {
@@ -580,11 +565,7 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
   // one 4-channel group of the conv input at (iy, ix), with the fill-mode view applied
   auto ldc4 = [&](int c4, int iy, int ix) -> f32x4 {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-#ifdef ICA_ABLATE_FILL
-    if (false) {
-#else
     if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
-#endif
       if constexpr ((FX & FX_UNSHUF) != 0) {
         // PixelUnshuffle(2): rho channel 16*c4g + 4*q + e of pixel (iy, ix) is channel 4*c4g + e
         // of the (2 Hin) x (2 Win) tensor at sub-pixel q = 2i + j
@@ -1002,12 +983,7 @@ ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb
         adv(ti_c, ch_c);
         bf16x8 b[PT];
 #pragma unroll
-#ifdef ICA_ABLATE_BLDS
-        for (int t = 0; t < PT; ++t) b[t] = cur[t];   // timing-only: no LDS operand reads (wrong results)
-        (void)po;
-#else
         for (int t = 0; t < PT; ++t) b[t] = f4_as_bf8(patch[po + t * 2 * UP_PC]);   // tile t: 2 rows down
-#endif
 #pragma unroll
         for (int t = 0; t < PT; ++t)
 #pragma unroll
@@ -1152,11 +1128,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int jt = wave & 1, nch = p.Cin / 16;
   // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
-#ifdef ICA_ABLATE_SAMECLASS
-  if (true) {  // timing-only: every wave runs the first class pair (4 waves share weights; wrong results)
-#else
   if (wave < 2) {
-#endif
     conv_up_pair<KS, 0, 0, 1, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   } else {
     conv_up_pair<KS, 0, 1, 1, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
@@ -1177,10 +1149,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
 // of one input pixel.  Weight fragments packed [it(3)][chunk][lane][8] with row
 // o = it*32 + (lane&31) = co*25 + ky*5 + kx.
 // --------------------------------------------------------------------------
-#ifndef ICA_T3_TH
-#define ICA_T3_TH 5
-#endif
-constexpr int T3_TH = ICA_T3_TH, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 238
+constexpr int T3_TH = 5, T3_TW = 32, T3_HR = T3_TH + 2, T3_HC = T3_TW + 2, T3_NPX = T3_HR * T3_HC;  // 238
 constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                                                // 8
 constexpr int T3_NCH_BF = 8;  // bf16 up-front-load path: Cin = 128
 constexpr int T3_BLOCKS = (2 * T3_ROWS * T3_NPX * 4 <= 160 * 1024) ? 2 : 1;
@@ -1474,7 +1443,6 @@ __global__ void pack_gdn_kernel(const float* __restrict__ gamma, const float* __
   }
 }
 
-#ifndef ICA_KERNELS_ONLY  // (kernel-only builds: register/scratch experiments on single instantiations)
 // --------------------------------------------------------------------------
 // Host launchers (C ABI)
 // --------------------------------------------------------------------------
@@ -1950,4 +1918,3 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
 }
 
 }  // extern "C"
-#endif  // ICA_KERNELS_ONLY

@@ -91,7 +91,7 @@ def _masked_mean(e, m):
 def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metric="L2",
            clamp=True, model="hyper", coupled=False, init_noise=None, eval_msssim=True,
            record=None, target=None, roi=None, la_tar=1.0, la_bkg_in=1.0, la_bkg_out=1.0, expensive=None,
-           adv=False):
+           adv=False, pad=None, padding_mode="reflect"):
     """attack_rd.attack_ restated (Adam on additive noise, L-inf box in the forward).
 
     record: optional list; per step appends dict(loss_i, branch) for trajectory tests.
@@ -105,9 +105,14 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
     """
     B = im_s.shape[0]
     with torch.no_grad():
-        res = codec.forward(P, im_s, model)
-        output_s = torch.clamp(res["x_hat"], 0.0, 1.0) if clamp else res["x_hat"]
         H, W = im_s.shape[2:]
+        if pad:   # attack_rd.py:389-419: padded pre-eval, cropped output_s, bits per unpadded pixel
+            import torch.nn.functional as F
+            res = codec.forward(P, F.pad(im_s, (pad, pad, pad, pad), mode=padding_mode), model)
+            output_s = torch.clamp(res["x_hat"][:, :, pad:-pad, pad:-pad], 0.0, 1.0)
+        else:
+            res = codec.forward(P, im_s, model)
+            output_s = torch.clamp(res["x_hat"], 0.0, 1.0) if clamp else res["x_hat"]
         bpp_ori = torch.stack([codec.bpp({k: v[b:b + 1] for k, v in res["likelihoods"].items()}, H * W)
                                for b in range(B)])
     noise_range = epsilon / 255.0
@@ -217,13 +222,17 @@ def _attack_roi(P, im_s, output_s, bpp_ori, steps, noise_range, noise_thr, lr, c
                            noise=noise.detach(), im_in=im_in, output_t=output_t, tar_mse=tar_mse)
 
 
-def ifgsm(P, im_s, steps=10, epsilon=16.0, momentum=False, model="hyper"):
-    """attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438) without random start, per image."""
+def ifgsm(P, im_s, steps=10, epsilon=16.0, momentum=False, model="hyper", start_noise=None):
+    """attack_ifgsm.attack_ifgsm (attack_ifgsm.py:364-438), per image.  start_noise: the U(-eps, eps) draw of
+    the random (PGD) start, im_adv0 = clamp(im_s + start_noise, 0, 1) (:377-380); None: start at im_s."""
     with torch.no_grad():
         res = codec.forward(P, im_s, model)
         output_s = torch.clamp(res["x_hat"], 0.0, 1.0)
     eps = epsilon / 255.0
-    im_adv = im_s.detach().clone().requires_grad_(True)
+    if start_noise is not None:
+        im_adv = torch.clamp(im_s + start_noise, 0, 1).detach().requires_grad_(True)
+    else:
+        im_adv = im_s.detach().clone().requires_grad_(True)
     g = torch.zeros_like(im_s)
     alpha = eps / steps
     for _ in range(steps):

@@ -1,7 +1,7 @@
 """Per-kernel timing of the bf16 conv kernels at BASELINE config-5 shapes (hyper q3, 8 x 2048x2048):
 level-1 (1024^2) <-> level-2 (512^2) layers and the RGB ends.  Median of 7 launches (HIP events, launch
 stream), printed with algorithmic TFLOP/s and the HBM bytes of the activation tensors they move.
-    python scripts/kbench_bf16.py [lib path] [--only name-substring]   (lib path: e.g. an ICA_ABLATE_* build)"""
+    python scripts/kbench_bf16.py [lib path] [--only name-substring]"""
 import os
 import sys
 

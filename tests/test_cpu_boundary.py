@@ -142,3 +142,40 @@ def test_header_compiles_as_c_and_cpp():
             pytest.skip(f"{cc} not available")
         r = subprocess.run([cc, "-fsyntax-only", "-x", lang, hdr], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
+
+
+def test_old_format_checkpoint_conversion(tmp_path, capsys):
+    """coder.load_model on an old-format checkpoint (coder.py:107-116): an anchors.balle.Image_coder state
+    dict ("net." prefix, CDF buffers of the checkpoint's size) is converted, re-saved as ckpt + "new" with a
+    "state_dict" key, and loaded; --eval on a training checkpoint reports epoch / step / lr (:138-146)."""
+    import torch
+    from imagecompression_adversarial_amd import coder
+    from imagecompression_adversarial_amd.anchors import model as am
+    src = am.init_model("hyper", 3, "mse", pretrained=False)
+    coder._synthetic_init(src, seed=3)
+    sd = src.state_dict()
+    sd["entropy_bottleneck._quantized_cdf"] = torch.arange(128 * 7, dtype=torch.int32).reshape(128, 7)
+    sd["entropy_bottleneck._offset"] = torch.full((128,), -3, dtype=torch.int32)
+    sd["entropy_bottleneck._cdf_length"] = torch.full((128,), 7, dtype=torch.int32)
+    old = {"net." + k: v for k, v in sd.items()}
+    path = str(tmp_path / "old.pth")
+    torch.save(old, path)
+    args = coder.config().parse_args(["-m", "hyper", "-q", "3", "-metric", "mse", "-ckpt", path, "-device", "cpu"])
+    net = coder.load_model(args, training=False)
+    got = net.state_dict()
+    for k, v in sd.items():
+        assert torch.equal(got[k].cpu(), v), k
+    new = torch.load(path + "new", weights_only=True)
+    assert set(new) == {"state_dict"} and set(new["state_dict"]) == set(sd)
+    # --eval on a training checkpoint
+    args2 = coder.config().parse_args(["-m", "hyper", "-q", "3", "-metric", "mse", "--synthetic-weights",
+                                       "-device", "cpu", "--adv"])
+    net2, _, opt, aux, sch = coder.load_model(args2, training=True)
+    torch.save({"epoch": 4, "step": 120, "state_dict": net2.state_dict(), "optimizer": opt.state_dict(),
+                "aux_optimizer": aux.state_dict(), "lr_scheduler": sch.state_dict()}, str(tmp_path / "train.pth"))
+    capsys.readouterr()
+    args3 = coder.config().parse_args(["-m", "hyper", "-q", "3", "-metric", "mse", "-ckpt", str(tmp_path / "train.pth"),
+                                       "-device", "cpu", "--eval", "--adv"])
+    coder.load_model(args3, training=False)
+    out = capsys.readouterr().out
+    assert "Trained epoch 4" in out and "Trained step 120" in out and "Learning rate: 0.0001" in out

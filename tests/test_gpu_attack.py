@@ -279,3 +279,54 @@ def test_branch_compaction_bitexact():
     cheap = [sum(br[b] for br in hist[0]) for b in range(3)]
     assert loops[0].census.tolist() == cheap
     assert loops[0].expensive_image_steps() == 90 - sum(cheap)
+
+
+def test_ifgsm_random_and_multi_start_vs_oracle(hyper3):
+    """attack_ifgsm random_start (PGD start, attack_ifgsm.py:377-380) with a shared U(-eps, eps) draw vs the
+    oracle; multi_start R keeps per image the restart with the largest vi (:434-437)."""
+    from types import SimpleNamespace
+    from imagecompression_adversarial_amd.attack_ifgsm import attack_ifgsm
+    from imagecompression_adversarial_amd.engine import CodecKernels
+    P = codec.perturb_params(codec.init_params("hyper", 3, seed=0), seed=1)
+    P["g_a.6.weight"] = P["g_a.6.weight"] * 40.0   # |y| ~ 1: the eval reconstruction moves, vi is defined
+    kern = CodecKernels({k: v.to(DEV) for k, v in P.items()}, "hyper")
+    x = rnd((2, 3, 64, 128), 72)
+    eps = 16 / 255.0
+    draws = [rnd((2, 3, 64, 128), 73 + r, -eps, eps) for r in range(3)]
+
+    class Net:
+        def kernels(self):
+            return kern
+    args = SimpleNamespace(steps=4, epsilon=16.0, clamp=True)
+    for momentum in (False, True):
+        xa, *_ = attack_ifgsm(x.to(DEV), Net(), args, random_start=True, momentum=momentum,
+                              start_noise=lambda r, shape: draws[r])
+        xr, _ = oatt.ifgsm(P, x, steps=4, momentum=momentum, start_noise=draws[0])
+        # attack_ifgsm returns the eval's clamp(im_adv, 0, 1) (attack_ifgsm.py:221,437)
+        diff = (xa.cpu() - torch.clamp(xr, 0, 1)).abs()
+        assert float((diff > 1e-6).float().mean()) < 1e-3
+        assert float(diff.max()) <= 2 * eps / 4 + 1e-6
+    res = attack_ifgsm(x.to(DEV), Net(), args, multi_start=3, momentum=True, start_noise=lambda r, shape: draws[r])
+    singles = [attack_ifgsm(x.to(DEV), Net(), args, random_start=True, momentum=True,
+                            start_noise=lambda r, shape, k=k: draws[k]) for k in range(3)]
+    for b in range(2):
+        vis = [s[7][b] for s in singles]
+        assert all(v is not None for v in vis)
+        k = max(range(3), key=lambda i: vis[i])
+        assert res[7][b] == vis[k]
+        assert torch.equal(res[0][b], singles[k][0][b])
+
+
+def test_pad_pre_eval_vs_oracle(hyper3):
+    """-p 32 -padmode reflect (attack_rd.py:389-419): the pre-eval codes the reflect-padded image; output_s is the
+    crop, bpp_ori the padded bits per unpadded pixel; the attack itself runs unpadded."""
+    from imagecompression_adversarial_amd.attack import attack_batch
+    P, kern = hyper3
+    x = rnd((2, 3, 64, 128), 81)
+    res = attack_batch(kern, x.to(DEV), steps=3, pad=32, eval_msssim=False)
+    ref = oatt.attack(P, x, steps=3, pad=32, eval_msssim=False)
+    assert rel_err(res.output_s.cpu(), ref.output_s) < 1e-4
+    assert torch.allclose(res.bpp_ori.cpu(), ref.bpp_ori, rtol=1e-4, atol=1e-5)
+    assert rel_err(res.noise.cpu(), ref.noise) < 2e-3
+    with pytest.raises(ValueError):
+        attack_batch(kern, x.to(DEV), steps=1, pad=8)
