@@ -141,6 +141,117 @@ def _bf16_tags(kern):
     return tags
 
 
+def _dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("ICA_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return world, rank, dev, dist
+
+
+def _kernel_table(hook, flops_img):
+    tot_ms = {tag: sum(a.elapsed_time(b) for a, b, _ in evs) for tag, evs in hook.items()}
+    tot_fl = {tag: sum(flops_img[tag] * n for _, _, n in evs) for tag, evs in hook.items()}
+    return tot_ms, tot_fl
+
+
+def bench_finetune(args):
+    """configs[3]: train.py --adv (train.py:335-366) outer steps on this rank's shard: the batch-coupled
+    300-step inner attack (a 4-byte all-reduce per inner step), the train-mode RD forward / backward with
+    every weight gradient, one flat gradient all-reduce (RCCL over xGMI), clip + Adam + aux Adam.
+    Weak scaling: 8 images of 256x256 per GPU (train.py's batch of 8 per rank), hyper q1, ms-ssim
+    (the README's fine-tune command), lambda from the train.py table."""
+    from types import SimpleNamespace
+    world, rank, dev, dist = _dist_env()
+    from imagecompression_adversarial_amd import codec as models
+    from imagecompression_adversarial_amd import coder
+    from imagecompression_adversarial_amd import dist as D
+    from imagecompression_adversarial_amd import hip_ops as K
+    from imagecompression_adversarial_amd.train import LAMBS, adv_step
+    from imagecompression_adversarial_amd.train_engine import RDTrainer
+    q, metric = (args.quality or 1), "ms-ssim"
+    B, H, W, inner = 8, 256, 256, 300
+    torch.manual_seed(0)
+    net = models.bmshj2018_hyperprior(q)
+    coder._synthetic_init(net, seed=0)
+    net = net.to(dev).train()
+    opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=1e-4))
+    lmbda = LAMBS[metric][q - 1]
+    tr = RDTrainer(net, metric, lmbda)
+    group = dist.group.WORLD if dist else None
+    fargs = SimpleNamespace(steps=inner, epsilon=16.0, noise=1e-4, lr_attack=0.01, att_metric="L2", clamp=True,
+                            round_adv=False)
+    gen = torch.Generator(device=dev).manual_seed(rank)
+    xs = [torch.rand((B, 3, H, W), generator=gen, device=dev) for _ in range(args.warmup + args.steps)]
+    for i in range(args.warmup):
+        adv_step(net, tr, opt, aux, xs[i], fargs, group, world)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    K.EVENT_HOOK = {}
+    K.FLOPS_HOOK = {}
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        adv_step(net, tr, opt, aux, xs[i], fargs, group, world)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    hook, K.EVENT_HOOK = K.EVENT_HOOK, None
+    if dist:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    N, M = net.N, net.M
+    flops_img = {t: (K.FLOPS_HOOK[t] if t in K.FLOPS_HOOK else layer_flops(t, N, M, H, W, 1)) for t in hook}
+    tot_ms, tot_fl = _kernel_table(hook, flops_img)
+    dom = max(tot_ms, key=tot_ms.get)
+    wg = [t for t in tot_ms if t.endswith(".wgrad")]
+    wdom = max(wg, key=tot_ms.get) if wg else None
+
+    def roof(tag):
+        if tag is None:
+            return None
+        ach = tot_fl[tag] / (tot_ms[tag] * 1e-3) / 1e12
+        return {"bound": "mfma", "kernel": tag, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "launch_ms": round(tot_ms[tag] / len(hook[tag]), 4),
+                "flops_per_launch": tot_fl[tag] / len(hook[tag])}
+    ms_outer = el / args.steps * 1e3
+    value = B * world * inner * args.steps / el
+    if rank == 0:
+        out = {
+            "metric": "attack-step·images/sec, train.py --adv fine-tune (configs[3]): inner attack image-steps per "
+                      "second over whole outer steps (inner attack + RD train step + grad all-reduce + Adam)",
+            "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_outer, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (torch.rand 256x256 crops, seeded CompressAI-init weights)",
+            "config": {"workload": f"train.py --adv -m hyper -q {q} -metric {metric} -steps {inner} -lamb {lmbda}, "
+                                   f"{B} images/GPU of {W}x{H}, one outer step per timed step",
+                       "per_gpu_batch": B, "global_batch": B * world, "height": H, "width": W,
+                       "parallelism": f"data-parallel x{world}, one flat grad all-reduce per outer step"},
+            "outer_steps_per_s": round(args.steps / el, 4),
+            "roofline": roof(dom), "wgrad_roofline": roof(wdom),
+            "per_kernel_ms_total_per_outer_step": {k: round(v / args.steps, 3) for k, v in sorted(tot_ms.items())},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,9 +264,10 @@ def main():
     ap.add_argument("--model", default="hyper", choices=("hyper", "cheng2020"))
     ap.add_argument("--precision", default=None, choices=("fp32", "bf16"),
                     help="conv operand precision of g_a/g_s (default fp32; bf16 for --config 5)")
-    ap.add_argument("--config", type=int, default=None, choices=(2, 3, 5),
+    ap.add_argument("--config", type=int, default=None, choices=(2, 3, 4, 5),
                     help="BASELINE.json configs[k-1] per-GPU shard: 2 hyper q3 fp32 (default), 3 cheng2020 q6, "
-                         "5 targeted ROI hyper q3 2048x2048 bf16")
+                         "4 train.py --adv fine-tune outer steps (8 x 256^2 per GPU, 300 inner steps, RCCL grad "
+                         "all-reduce), 5 targeted ROI hyper q3 2048x2048 bf16")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--full-run", dest="full_run", type=int, default=None,
@@ -163,6 +275,8 @@ def main():
                          "default 1 for the hyperprior configs at N = 1, 0 for cheng2020 (~7 min)")
     args = ap.parse_args()
 
+    if args.config == 4:
+        return bench_finetune(args)
     roi_mode = False
     if args.full_run is None:
         args.full_run = int(args.config != 3 and args.model != "cheng2020")

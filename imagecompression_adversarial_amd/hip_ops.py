@@ -459,16 +459,19 @@ def bits_to_bpp(sumlog: torch.Tensor, num_pixels: int) -> torch.Tensor:
 # --------------------------------------------------------------------------- #
 # Training-side wrappers (ica_train.hip)
 # --------------------------------------------------------------------------- #
-def wgrad(Sm4, A, Lg4, Bc, KS, S, out, accumulate=False):
-    """out[a][b][ky][kx] (+)= sum Sm[n][a][p] Lg[n][b][S p + k - KS//2]  (see include/ica_hip.h)."""
+def wgrad(Sm4, A, Lg4, Bc, KS, S, out, accumulate=False, tag=None):
+    """out[a][b][ky][kx] (+)= sum Sm[n][a][p] Lg[n][b][S p + k - KS//2]  (see include/ica_hip.h).
+    tag: optional EVENT_HOOK tag (algorithmic FLOPs 2 * A * B * KS^2 * small-grid pixels)."""
     N, _, Hs, Ws, _ = Sm4.shape
     _, _, Hb, Wb, _ = Lg4.shape
     if out.numel() != A * Bc * KS * KS or not out.is_contiguous():
         raise RuntimeError("wgrad: output must be a contiguous [A][B][KS][KS] tensor")
     nsplit = int(lib().ica_wgrad_nsplit(A, Bc, N * Hs * ((Ws + 31) // 32)))
     ws = torch.empty(int(lib().ica_wgrad_ws_size(A, Bc, KS, nsplit)), device=Sm4.device)
+    ev = _ev_begin(tag, N)
     call("ica_wgrad", ptr(Sm4), ptr(Lg4), ptr(ws), ptr(out), N, A, Bc, Hs, Ws, Hb, Wb, KS, S, KS // 2, nsplit,
          int(accumulate), stream())
+    _ev_end(ev, 2.0 * A * Bc * KS * KS * N * Hs * Ws)
     return out
 
 

@@ -58,7 +58,7 @@ def synthesis_backward(ex, g4, y_in4, saved, params, grads, prefix):
         p = ex.convs[i]
         cin = M if i == 0 else N
         inp = y_in4 if i == 0 else saved[i - 1][0]
-        K.wgrad(inp, cin, g, C, 5, 2, grads[f"{prefix}{2 * i}.weight"])
+        K.wgrad(inp, cin, g, C, 5, 2, grads[f"{prefix}{2 * i}.weight"], tag=f"{prefix}{2 * i}.wgrad")
         K.channel_sum(g, C, grads[f"{prefix}{2 * i}.bias"])
         if i > 0:
             t = torch.empty_like(saved[i - 1][0])
@@ -81,7 +81,7 @@ def analysis_backward(ex, gy4, x4, saved, params, grads, prefix, input_grad=Fals
     for i in (3, 2, 1, 0):
         inp = x4 if i == 0 else saved[i - 1][0]
         cin = 3 if i == 0 else N
-        K.wgrad(g, C, inp, cin, 5, 2, grads[f"{prefix}{2 * i}.weight"])
+        K.wgrad(g, C, inp, cin, 5, 2, grads[f"{prefix}{2 * i}.weight"], tag=f"{prefix}{2 * i}.wgrad")
         K.channel_sum(g, C, grads[f"{prefix}{2 * i}.bias"])
         if i > 0:
             t = torch.empty_like(saved[i - 1][0])
