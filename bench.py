@@ -129,16 +129,21 @@ def cpu_baseline(H, W, quality, seconds, model="hyper", big_batch=32):
                                                       "sample": f"1 step of {big_batch} images ({eb:.1f} s)"}}}
 
 
-def _bf16_tags(kern):
-    """Tags of the conv launches that run on bf16 operands (the roofline peak for those is BF16 MFMA)."""
-    tags = set()
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0   # fp32-equivalent ceiling of six bf16 MFMAs per fp32 k-step
+
+
+def _tag_prec(kern):
+    """Operand precision of each tagged conv launch (0 fp32 MFMA, 1 bf16, 2 bf16x6 fp32-accurate)."""
+    out = {}
     for tr, pre in ((kern.ga, "g_a"), (kern.gs, "g_s")):
         for i, p in enumerate(tr.convs):
-            if p.fwd_prec:
-                tags.add(f"{pre}.{2 * i}.fwd")
-            if p.bwd_prec:
-                tags.add(f"{pre}.{2 * i}.dgrad")
-    return tags
+            out[f"{pre}.{2 * i}.fwd"] = p.fwd_prec
+            out[f"{pre}.{2 * i}.dgrad"] = p.bwd_prec
+    return out
+
+
+def _peak(prec):
+    return {1: BF16_MFMA_PEAK_TFLOPS, 2: X6_PEAK_TFLOPS}.get(prec, FP32_MFMA_PEAK_TFLOPS)
 
 
 def _dist_env():
@@ -262,8 +267,9 @@ def main():
     ap.add_argument("--width", type=int, default=768)
     ap.add_argument("--quality", type=int, default=None, help="default 3 (hyper) / 6 (cheng2020)")
     ap.add_argument("--model", default="hyper", choices=("hyper", "cheng2020"))
-    ap.add_argument("--precision", default=None, choices=("fp32", "bf16"),
-                    help="conv operand precision of g_a/g_s (default fp32; bf16 for --config 5)")
+    ap.add_argument("--precision", default=None, choices=("fp32", "x6", "bf16"),
+                    help="conv operand precision of g_a/g_s: fp32 (fp32-operand MFMA), x6 (fp32-accurate bf16x6 "
+                         "split-operand MFMA), bf16 (config 5 default)")
     ap.add_argument("--config", type=int, default=None, choices=(2, 3, 4, 5),
                     help="BASELINE.json configs[k-1] per-GPU shard: 2 hyper q3 fp32 (default), 3 cheng2020 q6, "
                          "4 train.py --adv fine-tune outer steps (8 x 256^2 per GPU, 300 inner steps, RCCL grad "
@@ -371,7 +377,8 @@ def main():
     dom_ms = per_tag[dom] if dom else 0.0
     dom_flops = tot_fl[dom] / len(hook[dom]) if dom else 0.0
     achieved = tot_fl[dom] / (tot_ms[dom] * 1e-3) / 1e12 if dom else 0.0
-    peak = BF16_MFMA_PEAK_TFLOPS if (args.precision == "bf16" and dom in _bf16_tags(kern)) else FP32_MFMA_PEAK_TFLOPS
+    tag_prec = _tag_prec(kern) if model == "hyper" else {}
+    peak = _peak(tag_prec.get(dom, 0))
     # HBM bytes per launch of the dominant kernel from the committed PMC passes of the same shapes
     # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)
     traffic = None
@@ -421,7 +428,9 @@ def main():
             "metric": metric, "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 operands, f32 accumulate" if args.precision == "bf16" else "f32",
+            "dtype": {"bf16": "bf16 operands, f32 accumulate",
+                      "x6": "f32 (fp32-accurate: exact 3-way bf16 operand splits, 6 MFMA products, f32 accumulate)",
+                      }.get(args.precision, "f32"),
             "data": "synthetic (torch.rand images, seeded CompressAI-init weights)",
             "config": {"workload": (f"attack_rd -m {name} -q {args.quality} -att_metric L2 -noise 1e-4"
                                     + (f" -t <target> --mask_loc {W // 4} {3 * W // 4} {H // 4} {3 * H // 4}"
@@ -440,7 +449,7 @@ def main():
             "step_gflop_per_image": round(total_flops / B / 1e9, 2),
             "step_tflops": round(total_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 /
-                                        (BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS),
+                                        _peak({"bf16": 1, "x6": 2}.get(args.precision, 0)),
                                         4),
             "per_kernel_ms": {k: round(v, 4) for k, v in sorted(per_tag.items())},
             "cpu_baseline": cpu,

@@ -20,464 +20,7 @@
 //               parity classes (9/6/6/4 taps).  Block = 8x32 output pixels
 //               (4x16 per class); the whole-Cin input patch lives in LDS; each
 //               wave runs two class tiles paired 9+4 / 6+6 for balance.
-#include "ica_common.h"
-
-enum {
-  EPI_BIAS = 0,      // y = acc + bias
-  EPI_RELU = 1,      // y = relu(acc + bias)
-  EPI_GDN = 2,       // x = acc + bias; y = x * rsqrt(beta' + gamma' x^2)
-  EPI_IGDN = 3,      // x = acc + bias; y = x * sqrt(beta' + gamma' x^2)
-  EPI_GDN_BWD = 4,   // acc = dL/dy of a GDN; emit dL/dx  (needs saved y, s)
-  EPI_IGDN_BWD = 5,  // same for IGDN
-  EPI_LRELU = 6,     // y = leaky_relu(acc + bias, 0.01)
-  EPI_LRELU_BWD = 7, // y = acc * (m > 0 ? 1 : 0.01), m = in_x (the saved leaky-ReLU output)
-};
-// Compile-time feature flags (template parameter FX) so that plain layers compile to plain code:
-enum { FX_RES = 1, FX_PS = 2, FX_MASK = 4, FX_UNSHUF = 8, FX_T = 16 };  // FX_T: GDN-bwd writes save_t
-// Optional extras (present only in FX-enabled instantiations; res / save_x may still be null there):
-//   res      forward epilogues: y = act(...) + res (residual add after the activation);
-//            GDN_BWD/IGDN_BWD: acc += res before the GDN backward (gradient of out = gdn + skip)
-//   save_x   forward: the activation output before the residual add (GDN: y = x*s; LRELU: a);
-//            GDN_BWD/IGDN_BWD: the summed upstream gradient acc + res (feeds the skip branch)
-//   ps       (BIAS/RELU/LRELU) PixelShuffle(2) store: MFMA row rho = 16*c4 + 4*q + e is output
-//            channel 4*c4 + e at sub-pixel q = 2i + j of the (2 Hout) x (2 Wout) output
-//            (the host packs weights / bias in rho order)
-
-struct ConvParams {
-  const float* x;     // input  nChw4c [N][ceil(Cin/4)][Hin][Win][4]
-  float* y;           // output nChw4c [N][ceil(Cout/4)][Hout][Wout][4]
-  const float* wp;    // packed weight fragments (ica_pack_conv_weight)
-  const float* bias;  // [Cout] or null
-  const float* gp;    // packed gamma' fragments (fwd: gamma', bwd: gamma'^T)
-  const float* beta;  // beta' [Cout] (fwd GDN epilogues)
-  float* save_x;      // fwd GDN: pre-normalisation activation (optional)
-  float* save_s;      // fwd GDN: s = rsqrt(n) | sqrt(n)           (optional)
-  const float* in_x;  // bwd GDN: saved GDN OUTPUT y = x*s (x is recovered as y/s)
-  const float* in_s;  // bwd GDN: saved s
-  int N, Cin, Hin, Win, Cout, Hout, Wout;
-  float* save_t;      // bwd GDN (training): dL/dn per element, for the GDN parameter gradients
-  const float* res;   // optional residual (output layout), see above
-  const float* mask;  // conv_down fill_mode 1: leaky-ReLU mask source (input layout)
-  int fill_mode;      // conv_down: 0 plain, 1 x * lrelu'(mask), 2 PixelUnshuffle(2) view of x
-  int ps;             // PixelShuffle(2) store (BIAS/RELU/LRELU epilogues)
-  int prec;           // 0: fp32 operands (v_mfma_f32_32x32x2_f32, exact fp32 products)
-                      // 1: bf16 operands, fp32 accumulate (v_mfma_f32_32x32x16_bf16); wp / gp hold the
-                      //    bf16 packs (ica_pack_conv_weight_bf16 / ica_pack_gdn_bf16)
-};
-
-// --------------------------------------------------------------------------
-// Epilogue: acc[it] holds channels co_base + it*32 + acc_row(r,h) of pixel
-// (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
-// float4 of channel group c4 = co_base/4 + it*8 + 2g + h.
-// --------------------------------------------------------------------------
-template <int IT, int EPI, int FX, bool BF = false>
-ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
-                           bool valid, int co_base) {
-  const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int C4o = (p.Cout + 3) >> 2;
-  const unsigned plane = (unsigned)p.Hout * p.Wout;
-  const unsigned pix = valid ? ((unsigned)oy * p.Wout + ox) : 0u;
-  const size_t img = (size_t)C4o * plane;  // channel quads per image of every output-layout tensor
-  // channel group c4 = u + h (u = co_base/4 + it*8 + 2g, wave-uniform): quad offset = vo + so(u)
-  // (BF: every activation tensor of the epilogue is bf16 nChw4c, Img4T<true>)
-  using Img = Img4T<BF>;
-  const unsigned vo = h * plane + pix;
-  auto so = [&](int u) -> unsigned { return (unsigned)u * plane; };
-  const int cu = co_base >> 2;
-
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_LRELU) {
-    const Img Y(p.y, img, n);
-    // PixelShuffle(2) store: output tensor [N][Cout/16][2 Hout][2 Wout][4]; rho-row quad (it, g, h) is
-    // channel group c4 = (cu + it*8 + 2g) / 4 at sub-pixel q = 2(g&1) + h of the (2Hout)x(2Wout) plane
-    const unsigned plane2 = 4u * plane;
-    const unsigned vo_ps = valid ? ((unsigned)(2 * oy) * (2 * p.Wout) + 2 * ox + h) : 0u;
-    auto so_ps = [&](int it, int g) -> unsigned {
-      const int c4 = (cu + it * 8 + 2 * g) >> 2;
-      return (unsigned)c4 * plane2 + (unsigned)(g & 1) * (2 * p.Wout);
-    };
-    // (the shuffled tensor holds the same Cout * Hout * Wout floats per image as the plain one)
-    const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n);
-    const Img RS((FX & FX_RES) ? p.res : nullptr, img, n);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c0 = co_base + it * 32 + 8 * g + 4 * h;
-        if (c0 >= p.Cout) continue;
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = acc[it][4 * g + e];
-          if (c0 + e < p.Cout) {
-            if (p.bias) t += p.bias[c0 + e];
-          } else {
-            t = 0.f;
-          }
-          if constexpr (EPI == EPI_RELU) t = fmaxf(t, 0.f);
-          if constexpr (EPI == EPI_LRELU) t = t > 0.f ? t : t * 0.01f;
-          v[e] = t;
-        }
-        if (valid) {
-          unsigned vv, ss;
-          if constexpr ((FX & FX_PS) != 0) {
-            vv = vo_ps;
-            ss = so_ps(it, g);
-          } else {
-            vv = vo;
-            ss = so(cu + it * 8 + 2 * g);
-          }
-          if constexpr ((FX & FX_RES) != 0) {
-            if (p.save_x) SX.st(vv, ss, v);
-            if (p.res) {
-              const f32x4 r = RS.ld(vv, ss);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += r[e];
-            }
-          }
-          Y.st(vv, ss, v);
-        }
-      }
-    }
-  } else if constexpr (EPI == EPI_LRELU_BWD) {
-    const Img Y(p.y, img, n), M(p.in_x, img, n);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c0 = co_base + it * 32 + 8 * g + 4 * h;
-        if (c0 >= p.Cout || !valid) continue;
-        const unsigned ss = so(cu + it * 8 + 2 * g);
-        const f32x4 m = M.ld(vo, ss);
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float t = acc[it][4 * g + e];
-          v[e] = (c0 + e < p.Cout) ? (m[e] > 0.f ? t : t * 0.01f) : 0.f;
-        }
-        Y.st(vo, ss, v);
-      }
-    }
-  } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
-    // requires IT*32 == Cout, co_base == 0.  acc := x = conv + bias (kept intact
-    // until every normaliser tile is done); one 32-channel tile of
-    // n = beta' + gamma' x^2 at a time (16 accumulator registers live).
-    const Img Y(p.y, img, n), SS(p.save_s, img, n);
-    const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n), RS((FX & FX_RES) ? p.res : nullptr, img, n);
-#pragma unroll
-    for (int it = 0; it < IT; ++it)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
-    // bf16 path: x^2 (rounded to bf16) as the B operand of a bf16 GEMM with gamma' (its bf16 hi part; one
-    // MFMA per k-step); the accumulator registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives
-    // the matching gamma' order).  n = beta' + sum of non-negative terms then carries <= 2^-8 relative error,
-    // s and y half of it: the size of the bf16 rounding of the stored y and s.
-    bf16x8 xh[BF ? IT : 1][2];
-    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
-    if constexpr (BF) {
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xv = acc[it][8 * s + j];
-            xh[it][s][j] = (__bf16)(xv * xv);
-          }
-    }
-#pragma unroll
-    for (int ct = 0; ct < IT; ++ct) {
-      f32x16 nacc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) nacc[r] = p.beta[ct * 32 + acc_row(r, h)];
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        if constexpr (BF) {
-          const int o = (ct * IT + it) * 4096;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) nacc = mfma32bf(ld_bf8(grs, lane * 16, o + s * 2048), xh[it][s], nacc);
-        } else {
-          const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
-          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float xv = acc[it][r];
-            nacc = mfma32(ga[r], xv * xv, nacc);
-          }
-        }
-      }
-      if (valid) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 yv, sv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float nv = nacc[4 * g + e];
-            // bf16 path: v_rsq_f32 / v_sqrt_f32 (1 ulp; n >= beta' > 0), no IEEE division / sqrt fix-ups
-            float s;
-            if constexpr (BF) s = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
-            else s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
-            sv[e] = s;
-            yv[e] = acc[ct][4 * g + e] * s;
-          }
-          const unsigned ss = so(ct * 8 + 2 * g);
-          if (p.save_s) SS.st(vo, ss, sv);
-          if constexpr ((FX & FX_RES) != 0) {
-            if (p.save_x) SX.st(vo, ss, yv);
-            if (p.res) {
-              const f32x4 r = RS.ld(vo, ss);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) yv[e] += r[e];
-            }
-          }
-          Y.st(vo, ss, yv);
-        }
-      }
-    }
-  } else {  // EPI_GDN_BWD / EPI_IGDN_BWD, requires IT*32 == Cout
-    // acc = g = dL/dy.  t = (g x) dS/dn (GDN: -0.5 s^3, IGDN: 0.5/s) for all
-    // channel tiles, then per output tile jt: u = gamma'^T t (16 live
-    // accumulators) and dx = g s + 2 x u with x, s re-read (L2-hot).
-    // Residual gradient: added unconditionally (r = 0 without one) so that the accumulators are
-    // never live in two versions across a branch (that doubled the register footprint).
-    const Img Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
-    if constexpr (BF) {
-      // bf16 path (FX == 0, IT <= 4): ONE pass over the saved (y, s) — the second read of them was the
-      // epilogue's latency cost at 2 waves/SIMD.  Per element: t (-> a bf16 B fragment), g*s in place of g,
-      // and 2x = 2 y rcp(s) kept as bf16 (the saved y and s are bf16 already); then per output tile
-      // u = gamma'^T t (bf16 MFMAs, gamma' hi part) and dx = g s + 2x u, stores only.  t, gamma' and 2x rounded
-      // to bf16 add 2^-9-relative errors, the size of the bf16 storage of y and s.
-      static_assert(!BF || (FX == 0 && IT <= 4), "bf16 GDN-bwd epilogue: plain, IT <= 4");
-      bf16x8 th[IT][2];
-      u32x2 x2q[IT][4];
-      // unconditional loads (one basic block, all in flight): a pixel outside the output reads past the
-      // descriptor's range (returns 0); its MFMA column (lanes j, j+32 = one pixel) is never stored
-      const unsigned vo_ld = valid ? vo : 0x1FFFFFF0u;
-      __builtin_amdgcn_sched_barrier(0);  // not into the main loop (its weight ring is live there)
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const unsigned ss = so(it * 8 + 2 * g);
-          const f32x4 yv = IX.ld(vo_ld, ss), sv = IS.ld(vo_ld, ss);
-          f32x4 x2;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gg = acc[it][4 * g + e], sg = sv[e], yg = yv[e];
-            const float r = __builtin_amdgcn_rcpf(sg);
-            const float t = (EPI == EPI_GDN_BWD) ? (-0.5f * (gg * yg)) * (sg * sg) : (0.5f * (gg * yg)) * (r * r);
-            th[it][g >> 1][4 * (g & 1) + e] = (__bf16)t;
-            float gs = gg * sg;
-            asm volatile("" : "+v"(gs));  // materialise here: LLVM otherwise sinks g*s and y*rcp(s) into the
-            acc[it][4 * g + e] = gs;      // stores after the GEMM, keeping g, s, y, r live (spills)
-            x2[e] = 2.0f * (yg * r);
-          }
-          u32x2 q = f4_to_bf4(x2);
-          asm volatile("" : "+v"(q));
-          x2q[it][g] = q;
-        }
-      __builtin_amdgcn_sched_barrier(0);  // pack 2x here, do not sink y and rcp(s) into the second phase
-      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
-#pragma unroll
-      for (int jt = 0; jt < IT; ++jt) {
-        // keep each output tile's gamma'^T fragment loads inside its tile (hoisting all of them spilled)
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 uacc = f32x16{0};
-#pragma unroll
-        for (int ct = 0; ct < IT; ++ct) {
-          const int o = (jt * IT + ct) * 4096;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) uacc = mfma32bf(ld_bf8(grs, lane * 16, o + s * 2048), th[ct][s], uacc);
-        }
-        if (valid) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 x2 = bf4_to_f4(x2q[jt][g]);
-            f32x4 v;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + x2[e] * uacc[4 * g + e];
-            Y.st(vo, so(jt * 8 + 2 * g), v);
-          }
-        }
-      }
-    } else if constexpr (FX == 0 && IT <= 4) {
-      // fp32, plain layers: one pass over the saved (y, s) as well.  x = y / s, t and g*s are formed with the
-      // ops of the two-pass form below and kept in registers (gs in place of g), so dx needs no second read.
-      f32x16 tt[IT], xx[IT];
-      const unsigned vo_ld = valid ? vo : 0x0FFFFFF0u;  // past the descriptor's range: loads return 0
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const unsigned ss = so(it * 8 + 2 * g);
-          const f32x4 yv = IX.ld(vo_ld, ss), sv = IS.ld(vo_ld, ss);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float sg = sv[e], xs = yv[e] / sg;
-            const float gx = acc[it][4 * g + e] * xs;
-            tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
-            float gs = acc[it][4 * g + e] * sg;
-            float x2 = 2.0f * xs;
-            asm volatile("" : "+v"(gs), "+v"(x2));  // materialise (see the bf16 branch)
-            acc[it][4 * g + e] = gs;
-            xx[it][4 * g + e] = x2;
-          }
-        }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int jt = 0; jt < IT; ++jt) {
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 uacc = f32x16{0};
-#pragma unroll
-        for (int ct = 0; ct < IT; ++ct) {
-          const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
-          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
-#pragma unroll
-          for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
-        }
-        if (valid) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 v;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + xx[jt][4 * g + e] * uacc[4 * g + e];
-            Y.st(vo, so(jt * 8 + 2 * g), v);
-          }
-        }
-      }
-    } else {
-      if constexpr ((FX & FX_RES) != 0) {
-        const Img SX(p.save_x, img, n), RS(p.res, img, n);
-  #pragma unroll
-        for (int it = 0; it < IT; ++it)
-  #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const unsigned ss = so(it * 8 + 2 * g);
-            f32x4 r = {0.f, 0.f, 0.f, 0.f};
-            if (p.res && valid) r = RS.ld(vo, ss);
-  #pragma unroll
-            for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
-            if (p.save_x && valid)
-              SX.st(vo, ss, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
-          }
-      }
-      // IT > 4 (C = 192): g*s is parked in the output (same-thread global write, re-read below) so that
-      // the 6 accumulator tiles are dead while the 6 t tiles and the u GEMM are live.
-      constexpr bool STASH = IT > 4;
-      if constexpr (STASH) {
-        if (valid) {
-  #pragma unroll
-          for (int it = 0; it < IT; ++it)
-  #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const unsigned ss = so(it * 8 + 2 * g);
-              const f32x4 sv = IS.ld(vo, ss);
-              Y.st(vo, ss, f32x4{acc[it][4 * g] * sv[0], acc[it][4 * g + 1] * sv[1], acc[it][4 * g + 2] * sv[2],
-                                 acc[it][4 * g + 3] * sv[3]});
-            }
-        }
-      }
-      // t = (g x) dS/dn with x = y / s (in_x holds the GDN output y).  fp32 path: IEEE divisions, the op order
-      // the parity tests were pinned with.  bf16 path: GDN -0.5 g y s^2, IGDN 0.5 g y rcp(s)^2 (v_rcp_f32; the
-      // epilogue was VALU-bound on division sequences), and t goes straight into its hi/lo B fragments
-      // (register r = 4g+e is k-step r>>3, element r&7), no fp32 copy kept.
-      f32x16 tt[BF ? 1 : IT];
-      bf16x8 th[BF ? IT : 1][2], tl[BF ? IT : 1][2];
-      const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
-  #pragma unroll
-      for (int it = 0; it < IT; ++it)
-  #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const unsigned ss = so(it * 8 + 2 * g);
-          f32x4 xv = {0.f, 0.f, 0.f, 0.f}, sv = {1.f, 1.f, 1.f, 1.f};
-          if (valid) {
-            xv = IX.ld(vo, ss);
-            sv = IS.ld(vo, ss);
-          }
-          f32x4 tv;
-  #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float s = sv[e];
-            float t;
-            if constexpr (!BF) {
-              const float gx = acc[it][4 * g + e] * (xv[e] / s);
-              t = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (s * s * s) : gx / (2.0f * s);
-            } else if constexpr (EPI == EPI_GDN_BWD) {
-              t = (-0.5f * (acc[it][4 * g + e] * xv[e])) * (s * s);
-            } else {
-              const float r = __builtin_amdgcn_rcpf(s);
-              t = (0.5f * (acc[it][4 * g + e] * xv[e])) * (r * r);
-            }
-            tv[e] = t;
-            if constexpr (BF) {
-              __bf16 hi, lo;
-              split_bf(t, hi, lo);
-              th[it][g >> 1][4 * (g & 1) + e] = hi;
-              tl[it][g >> 1][4 * (g & 1) + e] = lo;
-            } else {
-              tt[it][4 * g + e] = t;
-            }
-          }
-          if constexpr ((FX & FX_T) != 0) {
-            if (valid) ST.st(vo, ss, tv);
-          }
-        }
-      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
-  #pragma unroll
-      for (int jt = 0; jt < IT; ++jt) {
-        f32x16 uacc = f32x16{0};
-  #pragma unroll
-        for (int ct = 0; ct < IT; ++ct) {
-          if constexpr (BF) {
-            const int o = (jt * IT + ct) * 4096;
-  #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const bf16x8 ah = ld_bf8(grs, lane * 16, o + s * 2048), al = ld_bf8(grs, lane * 16, o + s * 2048 + 1024);
-              uacc = mfma32bf(ah, th[ct][s], uacc);
-              uacc = mfma32bf(al, th[ct][s], uacc);
-              uacc = mfma32bf(ah, tl[ct][s], uacc);
-            }
-          } else {
-            const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
-            const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-            const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                                  g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
-  #pragma unroll
-            for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
-          }
-        }
-        if (valid) {
-  #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const unsigned ss = so(jt * 8 + 2 * g);
-            const f32x4 xv = IX.ld(vo, ss), sv = IS.ld(vo, ss);
-            f32x4 v;
-            // dx = g s + 2 x u,  x = y / s (bf16 path: y * rcp(s))
-            f32x4 xs;
-  #pragma unroll
-            for (int e = 0; e < 4; ++e) xs[e] = BF ? xv[e] * __builtin_amdgcn_rcpf(sv[e]) : xv[e] / sv[e];
-            if constexpr (STASH) {
-              const f32x4 gs = Y.ld(vo, ss);
-  #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = gs[e] + 2.0f * xs[e] * uacc[4 * g + e];
-            } else {
-  #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int r = 4 * g + e;
-                v[e] = acc[jt][r] * sv[e] + 2.0f * xs[e] * uacc[r];
-              }
-            }
-            Y.st(vo, ss, v);
-          }
-        }
-      }
-    }
-  }
-}
+#include "ica_conv_epi.h"
 
 // bf16 weight-fragment load of tile it at step g
 #define ICA_WLOAD_BF(w, it, g) ((w)[(it) * 64])
@@ -1678,6 +1221,9 @@ static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStre
   return -6;
 }
 
+// fp32-accurate bf16x6 operand kernels (ica_conv_x6.hip)
+int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, int epi, int fx, hipStream_t st);
+
 // C-ABI argument block of ica_conv_ex (mirrors include/ica_hip.h)
 extern "C" {
 typedef struct ica_conv_args {
@@ -1903,7 +1449,7 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   ConvParams p{a->x,    a->y,    a->wp,   a->bias, a->gp,   a->beta, a->save_x, a->save_s, a->in_x, a->in_s,
                a->N,    a->Cin,  a->Hin,  a->Win,  a->Cout, a->Hout, a->Wout,   a->save_t, a->res,  a->mask,
                a->fill_mode, a->ps, a->prec};
-  if (a->prec != 0 && a->prec != 1) return -4;
+  if (a->prec != 0 && a->prec != 1 && a->prec != 2) return -4;
   const int it = resolve_it(a->Cout, a->it);
   if (a->epi >= EPI_GDN && a->epi <= EPI_IGDN_BWD && a->Cout != it * 32) return -4;
   if (a->ps && (a->Cout % 16 != 0 || !(a->epi == EPI_BIAS || a->epi == EPI_RELU || a->epi == EPI_LRELU))) return -4;
@@ -1912,6 +1458,7 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   if (a->epi == EPI_LRELU_BWD && !a->in_x) return -4;
   const int fx = ((a->res || a->save_x) ? FX_RES : 0) | (a->ps ? FX_PS : 0) | (a->fill_mode == 1 ? FX_MASK : 0) |
                  (a->fill_mode == 2 ? FX_UNSHUF : 0) | (a->save_t ? FX_T : 0);
+  if (a->prec == 2) return ica_conv_x6_dispatch(p, a->kind, a->KS, a->S, it, a->epi, fx, st);
   if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, fx, st);
   if (a->kind == 1) return a->S == 2 ? pick_up(p, a->KS, it, a->epi, fx, st) : -6;
   return -6;

@@ -1,0 +1,438 @@
+// fp32-accurate convolutions on the bf16 matrix cores ("x6" operands), for the k5 s2 layers of the bmshj2018
+// analysis / synthesis transforms (anchors/utils.py:112-130) and their input gradients.
+//
+// CDNA4's fp32 MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of the bf16 rate.  Every fp32 operand is split exactly
+// into three bf16 parts, v = v_hi + v_mid + v_lo (each a round-to-nearest residual: 8 + 8 + 8 significant bits =
+// the fp32 significand), and a product is the six partial products with combined weight >= 2^-16:
+//     a*b ~ ah*bh + ah*bm + am*bh + ah*bl + al*bh + am*bm
+// (dropped: am*bl + al*bm + al*bl, below 2^-24 relative, the size of one fp32 rounding).  bf16 x bf16 products are
+// exact in the fp32 accumulator, which adds them as the fp32 MFMA adds its own products, so the result has fp32
+// accuracy (scripts/exp/x6_down.cpp: max |err| vs float64 2.3e-6 where a sequential fp32 FMA chain gives 3.1e-6).
+// Six v_mfma_f32_32x32x16_bf16 replace eight v_mfma_f32_32x32x2_f32 per 16-deep k step: 192 instead of 512 cycles.
+//
+// Storage stays fp32 (activations, saved tensors, gradients): the split happens when an input patch is staged into
+// LDS (three bf16 planes, 16-B entries of 8 channels) and, for the weights, once per weight version
+// (ica_pack_conv_weight_x6: three bf16 fragment planes).  The epilogues are the fp32 ones of ica_conv_epi.h.
+//
+//   conv_down_x6 : stride-2 5x5 conv.  Block = 4 waves x 2 pixel tiles x 32 px (8 x 32 outputs), IT x 32 output
+//                  channels; K loop = 16-channel LDS chunks x 25 taps, 6 x IT x 2 MFMAs per (chunk, tap).
+//   conv_up_x6   : ConvTranspose2d k5 s2 p2 op1 as 4 output-parity classes (9/6/6/4 taps).  Block = 8 x 16 input
+//                  pixels (16 x 32 outputs); the channel group (all of Cin, or 64-channel groups) lives in LDS;
+//                  each wave runs two classes (9 + 4 or 6 + 6 taps) over 2 pixel tiles.
+// One block per CU (the 3-plane patches take 122 / 138 KB of LDS), so each wave has the whole 512-register file.
+#include <type_traits>
+
+#include "ica_conv_epi.h"
+
+namespace {
+
+// v -> (hi, mid, lo) bf16 quads, each stage round-to-nearest-even on the residual (exact: hi + mid + lo == v)
+ICA_DEV void split3(f32x4 v, u32x2& hi, u32x2& mid, u32x2& lo) {
+  bf16x4 a, b, c;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    const float r1 = v[e] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    a[e] = h;
+    b[e] = m;
+    c[e] = (__bf16)r2;
+  }
+  hi = __builtin_bit_cast(u32x2, a);
+  mid = __builtin_bit_cast(u32x2, b);
+  lo = __builtin_bit_cast(u32x2, c);
+}
+
+// the six products of one 16-deep k step (small terms first)
+ICA_DEV f32x16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = mfma32bf(a[2], b[0], c);
+  c = mfma32bf(a[0], b[2], c);
+  c = mfma32bf(a[1], b[1], c);
+  c = mfma32bf(a[1], b[0], c);
+  c = mfma32bf(a[0], b[1], c);
+  c = mfma32bf(a[0], b[0], c);
+  return c;
+}
+
+constexpr int X6_PT = 2;                 // 32-pixel tiles per wave
+constexpr int XD_TW = 32, XD_TH = 4 * X6_PT;
+
+// --------------------------------------------------------------------------------------------------------------
+// conv_down_x6: weights [plane][cb][chunk][tap][it][lane] bf16x8 (plane stride ps fragments)
+// --------------------------------------------------------------------------------------------------------------
+template <int IT, int EPI>
+__global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long ps) {
+  constexpr int KS = 5, S = 2, PAD = 2, KK = 25, PT = X6_PT, TW = XD_TW, TH = XD_TH;
+  constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;
+  constexpr int NF = (4 * PLANE + 255) / 256, NB = (NF + 1) / 2;  // fill items per thread, in two batches
+  __shared__ f32x4 patch[3 * 2 * PLANE];                          // [plane][half][pixel]: 8 channels as bf16
+  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int Cin4 = (p.Cin + 3) >> 2, nch = (Cin4 * 4 + 15) / 16;
+  f32x16 acc[PT][IT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
+
+  // patch fill: 16-B buffer loads (32-bit offsets into this image; padding and channel quads past Cin read out of
+  // the descriptor's range and return zeros), split into the three planes.  The first batch is issued before the
+  // barrier that ends the previous chunk's reads.
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  auto batch = [&](int ch, int i0, f32x4 (&v)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = threadIdx.x + 256 * (i0 + i);
+      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+      const int iy = iy0 + pr, ix = ix0 + pc, c4 = ch * 4 + q;
+      const bool ok = i0 + i < NF && e < 4 * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+    }
+  };
+  auto put = [&](int i0, const f32x4 (&v)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = threadIdx.x + 256 * (i0 + i);
+      if (i0 + i < NF && e < 4 * PLANE) {
+        const int q = e / PLANE, pix = e - q * PLANE;
+        u32x2 a, b, c;
+        split3(v[i], a, b, c);
+        const int ent = (q >> 1) * PLANE + pix;
+        p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
+        p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+        p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+      }
+    }
+  };
+  auto fill = [&](int ch) {
+    f32x4 v[NB];
+    batch(ch, 0, v);
+    __syncthreads();
+    put(0, v);
+    batch(ch, NB, v);
+    put(NB, v);
+    __syncthreads();
+  };
+
+  const int total = nch * KK;
+  // weight fragments through one buffer descriptor: a per-lane byte offset and a wave-uniform (scalar) one
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * total * IT * 64;
+  auto ldw = [&](bf16x8 (&a)[IT][3], int g) {
+    const int f = wbase + min(g, total - 1) * IT * 64;
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+  };
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) {
+    const int ch = g / KK, tap = g - ch * KK;
+    if (tap == 0) fill(ch);
+    ldw(nxt, g + 1);  // one step ahead (ping-pong; a step is 6 x IT x PT MFMAs)
+    const int ky = tap / 5, kx = tap - ky * 5;
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int o = h * PLANE + (S * (wave * PT + t) + ky) * PC + S * j + kx;
+      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], b, acc[t][it]);
+    }
+  };
+  bf16x8 fa[IT][3], fb[IT][3];
+  ldw(fa, 0);
+  int g = 0;
+#pragma unroll 1
+  for (; g + 1 < total; g += 2) {
+    step(fa, fb, g);
+    step(fb, fa, g + 1);
+  }
+  if (g < total) step(fa, fb, g);
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int oy = oy0 + wave * PT + t, ox = ox0 + j;
+    conv_epilogue<IT, EPI, 0, false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  }
+}
+
+// --------------------------------------------------------------------------------------------------------------
+// conv_up_x6: weights [plane][cb][tap][chunk][it][lane] bf16x8.  Output y = 2a + PY uses taps ky = ky0 + 2i,
+// ky0 = (PY + 2) & 1, at input row a + (PY + 2 - ky) / 2 (conv_up_kernel's decomposition).
+// --------------------------------------------------------------------------------------------------------------
+constexpr int XU_TW = 16, XU_TH = 4 * X6_PT, XU_PC = XU_TW + 2, XU_PLANE = (XU_TH + 2) * XU_PC;  // 180 px
+
+template <int CG>
+constexpr int xu_lds_bytes() { return 3 * (CG / 8) * XU_PLANE * 16; }
+
+template <int PY, int PX, int IT, int CG>
+ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch, int grp, long ps,
+                              f32x16 (&acc)[X6_PT][IT]) {
+  constexpr int KS = 5, PAD = 2, PT = X6_PT;
+  constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
+  constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
+  constexpr int NCG = CG / 16;   // 16-channel chunks per LDS group
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * KS * KS * nch * IT * 64;
+  const int total = NT * NCG;
+  auto wofs = [&](int u) -> int {   // fragment set of (tap ti, chunk c) of this group
+    const int ti = u / NCG, c = u - ti * NCG;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    return (ky * KS + kx) * nch + grp * NCG + c;
+  };
+  auto ldw = [&](bf16x8 (&a)[IT][3], int u) {
+    const int f = wbase + wofs(min(u, total - 1)) * IT * 64;
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+  };
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int u) {
+    ldw(nxt, u + 1);
+    const int ti = u / NCG, c = u - ti * NCG;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
+    const int e = (2 * c + h) * XU_PLANE + pr * XU_PC + pc;
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int o = e + t * 2 * XU_PC;   // tile t: 2 input rows down
+      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[(CG / 8) * XU_PLANE + o]),
+                           f4_as_bf8(patch[2 * (CG / 8) * XU_PLANE + o])};
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], b, acc[t][it]);
+    }
+  };
+  bf16x8 fa[IT][3], fb[IT][3];
+  ldw(fa, 0);
+  int u = 0;
+#pragma unroll 1
+  for (; u + 1 < total; u += 2) {
+    step(fa, fb, u);
+    step(fb, fa, u + 1);
+  }
+  if (u < total) step(fa, fb, u);
+}
+
+template <int IT, int EPI, int CG>
+__global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long ps) {
+  constexpr int PT = X6_PT, NQ = CG / 4;
+  extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
+  const int tiles_x = (p.Win + XU_TW - 1) / XU_TW, tiles_y = (p.Hin + XU_TH - 1) / XU_TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int a0 = ty * XU_TH, b0 = tx * XU_TW;
+  const int Cin4 = p.Cin >> 2, nch = p.Cin / 16, ngrp = p.Cin / CG;
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  // one channel group into LDS: NQ quads x XU_PLANE pixels, batches of 8 loads per thread (forced inline: as a
+  // call it kept the whole register file live across an s_swappc)
+  auto fill = [&](int grp) __attribute__((always_inline)) {
+    constexpr int FB = 8, TOT = NQ * XU_PLANE;
+    __syncthreads();
+    for (int e0 = threadIdx.x; e0 < TOT; e0 += 256 * FB) {
+      f32x4 v[FB];
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        const int e = e0 + 256 * i;
+        const int q = e / XU_PLANE, rem = e - q * XU_PLANE, pr = rem / XU_PC, pc = rem - pr * XU_PC;
+        const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+        const bool ok = e < TOT && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+        const unsigned vo = ((unsigned)(grp * NQ + q) * xplane + (unsigned)iy * p.Win + ix) * 16u;
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        const int e = e0 + 256 * i;
+        if (e < TOT) {
+          const int q = e / XU_PLANE, pix = e - q * XU_PLANE;
+          u32x2 a, b, c;
+          split3(v[i], a, b, c);
+          const int ent = (q >> 1) * XU_PLANE + pix;
+          p2[(0 * (CG / 8) * XU_PLANE + ent) * 2 + (q & 1)] = a;
+          p2[(1 * (CG / 8) * XU_PLANE + ent) * 2 + (q & 1)] = b;
+          p2[(2 * (CG / 8) * XU_PLANE + ent) * 2 + (q & 1)] = c;
+        }
+      }
+    }
+    __syncthreads();
+  };
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int jt = wave & 1;
+  const int j = threadIdx.x & 31;
+  const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
+  // one class of the wave's pair: all channel groups (a group is re-staged per class when Cin > CG), then its
+  // epilogue; classes pair 9 + 4 and 6 + 6 taps for balance
+  auto run_class = [&](auto py_c, auto px_c, bool refill) __attribute__((always_inline)) {
+    constexpr int PY = decltype(py_c)::value, PX = decltype(px_c)::value;
+    f32x16 acc[PT][IT];
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
+    for (int grp = 0; grp < ngrp; ++grp) {
+      if (refill) fill(grp);
+      conv_up_x6_class<PY, PX, IT, CG>(p, patch, jt, cb, nch, grp, ps, acc);
+    }
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
+      conv_epilogue<IT, EPI, 0, false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  const bool multi = ngrp > 1;
+  if (!multi) fill(0);
+  // every wave joins every fill barrier: both classes of every wave run the same group sequence
+  if (wave < 2) {
+    run_class(I0{}, I0{}, multi);
+    run_class(I1{}, I1{}, multi);
+  } else {
+    run_class(I0{}, I1{}, multi);
+    run_class(I1{}, I0{}, multi);
+  }
+}
+
+// (cb, outer, inner, it, lane, s) fragment index of pack_conv_kernel (CC = 16) -> three split planes
+__global__ void pack_conv_x6_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int O, int C, int KS,
+                                    long so, long sc, int IT, int order, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int KK = KS * KS;
+  const int nch = (((C + 3) / 4) * 4 + 15) / 16;
+  long t = i;
+  const int s = t % 8; t /= 8;
+  const int lane = t % 64; t /= 64;
+  const int it = t % IT; t /= IT;
+  int inner, outer;
+  if (order == 0) { inner = t % KK; t /= KK; outer = t % nch; t /= nch; }
+  else { inner = t % nch; t /= nch; outer = t % KK; t /= KK; }
+  const int cb = (int)t;
+  const int chunk = order == 0 ? outer : inner;
+  const int tap = order == 0 ? inner : outer;
+  const int o = cb * IT * 32 + it * 32 + (lane & 31);
+  const int c = chunk * 16 + (lane >> 5) * 8 + s;
+  float v = 0.f;
+  if (o < O && c < C) v = w[o * so + c * sc + (tap / KS) * KS + (tap % KS)];
+  const __bf16 a = (__bf16)v;
+  const float r1 = v - (float)a;
+  const __bf16 b = (__bf16)r1;
+  dst[i] = a;
+  dst[total + i] = b;
+  dst[2 * total + i] = (__bf16)(r1 - (float)b);
+}
+
+template <int IT, int EPI>
+int launch_down_x6(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + XD_TH - 1) / XD_TH) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * ((((p.Cin + 3) / 4) * 4 + 15) / 16) * 25 * IT * 64;
+  hipLaunchKernelGGL((conv_down_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int IT, int EPI, int CG>
+int launch_up_x6(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + XU_TH - 1) / XU_TH) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * 25 * (p.Cin / 16) * IT * 64;
+  constexpr size_t lds = xu_lds_bytes<CG>();
+  static_assert(lds <= 160 * 1024, "conv_up_x6 channel group exceeds LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6_kernel<IT, EPI, CG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_up_x6_kernel<IT, EPI, CG>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int IT, int EPI>
+int pick_up_x6(const ConvParams& p, hipStream_t st) {
+  if (p.Cin <= 128 && p.Cin % 16 == 0) {
+    if (p.Cin == 128) return launch_up_x6<IT, EPI, 128>(p, st);
+    if (p.Cin == 64) return launch_up_x6<IT, EPI, 64>(p, st);
+    return -2;
+  }
+  if (p.Cin % 64 == 0) return launch_up_x6<IT, EPI, 64>(p, st);
+  return -2;
+}
+
+}  // namespace
+
+// x6 launches (ica_conv_ex with prec = 2): the k5 s2 conv (kind 0) and transposed conv (kind 1) layers of the
+// bmshj2018 transforms.  Returns -4 for shapes / epilogues without an x6 kernel (the caller keeps those fp32).
+int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, int epi, int fx, hipStream_t st) {
+  if (KS != 5 || S != 2 || fx != 0) return -4;
+  if (p.Cout % 32 != 0) return -4;
+  if (kind == 0) {
+    if (p.Cin < 16 || p.Hout * 2 != p.Hin + (p.Hin & 1) || p.Wout * 2 != p.Win + (p.Win & 1)) return -2;
+    if (it == 4) {
+      switch (epi) {
+        case EPI_BIAS: return launch_down_x6<4, EPI_BIAS>(p, st);
+        case EPI_GDN: return launch_down_x6<4, EPI_GDN>(p, st);
+        case EPI_IGDN_BWD: return launch_down_x6<4, EPI_IGDN_BWD>(p, st);
+        default: return -5;
+      }
+    }
+    if (it == 3 && epi == EPI_BIAS) return launch_down_x6<3, EPI_BIAS>(p, st);
+    return -3;
+  }
+  if (kind == 1) {
+    if (p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
+    if (it == 4) {
+      switch (epi) {
+        case EPI_BIAS: return pick_up_x6<4, EPI_BIAS>(p, st);
+        case EPI_IGDN: return pick_up_x6<4, EPI_IGDN>(p, st);
+        case EPI_GDN_BWD: return pick_up_x6<4, EPI_GDN_BWD>(p, st);
+        default: return -5;
+      }
+    }
+    return -3;
+  }
+  return -6;
+}
+
+extern "C" {
+
+size_t ica_pack_conv_weight_x6_size(int O, int C, int KS, int IT) {
+  const int ncb = (O + IT * 32 - 1) / (IT * 32);
+  const int nch = (((C + 3) / 4) * 4 + 15) / 16;
+  return (size_t)3 * ncb * nch * KS * KS * IT * 64 * 8;
+}
+
+// three bf16 planes (hi, mid, lo) of the 16-channel-chunk fragment pack; order 0: conv_down [cb][chunk][tap],
+// order 1: conv_up [cb][tap][chunk]
+int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
+                            hipStream_t st) {
+  if (it <= 0) return -3;
+  const long total = (long)ica_pack_conv_weight_x6_size(O, C, KS, it) / 3;
+  hipLaunchKernelGGL(pack_conv_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
+                     reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, it, order, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

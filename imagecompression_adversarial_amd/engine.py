@@ -193,13 +193,15 @@ class CodecKernels:
     """Whole-model executor from a CompressAI-format state dict (device tensors)."""
 
     def __init__(self, sd: dict, model: str = "hyper", precision: str = "fp32"):
-        """precision 'bf16': g_a / g_s run bf16-operand MFMA convs (fp32 accumulate, bf16x3 GDN normaliser;
-        BASELINE config 5); h_a / h_s and the entropy models stay fp32."""
+        """precision 'x6': the k5 s2 g_a / g_s layers run the fp32-accurate bf16x6 kernels (ica_conv_x6.hip: exact
+        3-way bf16 operand splits, six products, fp32 accumulate and fp32 epilogues / storage); 'fp32': fp32-operand
+        MFMA everywhere; 'bf16': bf16-operand MFMA convs (fp32 accumulate, bf16 activations; BASELINE config 5,
+        SURVEY §8f rank 1).  h_a / h_s and the entropy models stay fp32."""
         self.model = model
-        if precision not in ("fp32", "bf16"):
-            raise ValueError(f"precision {precision!r}: fp32 | bf16")
+        if precision not in ("fp32", "bf16", "x6"):
+            raise ValueError(f"precision {precision!r}: fp32 | x6 | bf16")
         self.precision = precision
-        prec = K.PREC_BF16 if precision == "bf16" else K.PREC_FP32
+        prec = {"fp32": K.PREC_FP32, "bf16": K.PREC_BF16, "x6": K.PREC_X6}[precision]
         if sd["g_a.0.weight"].device.type != "cuda":
             raise RuntimeError("CodecKernels needs the state dict on the HIP device")
         self.ga = Analysis(sd, prec=prec)

@@ -123,7 +123,29 @@ def pack_conv_bf16(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, 
     return dst
 
 
-PREC_FP32, PREC_BF16 = 0, 1
+PREC_FP32, PREC_BF16, PREC_X6 = 0, 1, 2
+
+
+def x6_it(O: int) -> int:
+    """Row tiles per wave of an x6 launch (the library default for O: 4 for 128 channels, 3 for 192)."""
+    return int(lib().ica_conv_it(O))
+
+
+def pack_conv_x6(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, order: int, it: int) -> torch.Tensor:
+    """fp32-accurate bf16x6 fragments (prec=2 launches, ica_conv_x6.hip): three bf16 planes (hi, mid, lo: an exact
+    split of each weight) of the CC=16 fragment order."""
+    w = w.detach().contiguous()
+    _dev_check(w, "weight")
+    n = int(lib().ica_pack_conv_weight_x6_size(O, Cc, KS, it))
+    dst = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    call("ica_pack_conv_weight_x6", ptr(w), ptr(dst), O, Cc, KS, so, sc, order, it, stream())
+    return dst
+
+
+def x6_ok(O: int, C: int, it: int) -> bool:
+    """Layers the x6 kernels cover: k5 s2, >= 16 input channels, 128 output channels (IT 4, every epilogue) or
+    96-multiples at IT 3 (bias), no explicit 6-tile (C = 192 GDN) launch."""
+    return it == 0 and C >= 16 and C % 16 == 0 and (O % 128 == 0 or O % 96 == 0) and (C <= 128 or C % 64 == 0)
 
 
 def conv_cc(Cin: int) -> int:
@@ -161,6 +183,9 @@ class PackedConv:
         self.it_fwd, self.it_bwd = it_fwd, it_bwd
         if prec == PREC_BF16 and (it_fwd or it_bwd):
             raise NotImplementedError("the bf16 conv path covers the N = 128 transforms (q1-5)")
+        if prec == PREC_X6:
+            self._init_x6(weight, bias, kind, stride)
+            return
         self.kind = kind
         self.fwd_prec = self.bwd_prec = PREC_FP32
         self.stride = stride
@@ -213,6 +238,29 @@ class PackedConv:
             raise ValueError(kind)
         self.bias = None if bias is None else bias.detach().contiguous()
 
+    def _init_x6(self, weight, bias, kind, stride):
+        """PREC_X6: the k5 s2 launches with >= 16 channels on both ends run on the bf16x6 kernels; the RGB ends
+        (3-channel conv input / transposed-conv output) and explicit 6-tile layers keep the fp32 packs."""
+        fp = PackedConv(weight, bias, kind, stride, PREC_FP32, self.it_fwd, self.it_bwd)
+        self.__dict__.update(fp.__dict__)
+        if self.KS != 5 or stride != 2:
+            return
+        KK = 25
+        if kind == "conv":
+            if x6_ok(self.Cout, self.Cin, self.it_fwd):     # forward conv_down: o = co, c = ci
+                self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN, x6_it(self.Cout))
+                self.fwd_prec = PREC_X6
+            if self.Cin != 3 and x6_ok(self.Cin, self.Cout, self.it_bwd):   # dgrad conv_up: o = ci, c = co
+                self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP, x6_it(self.Cin))
+                self.bwd_prec = PREC_X6
+        else:
+            if self.Cout != 3 and x6_ok(self.Cout, self.Cin, self.it_fwd):  # forward conv_up: o = co, c = ci
+                self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP, x6_it(self.Cout))
+                self.fwd_prec = PREC_X6
+            if x6_ok(self.Cin, self.Cout, self.it_bwd):       # dgrad conv_down: o = ci, c = co
+                self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, x6_it(self.Cin))
+                self.bwd_prec = PREC_X6
+
 
 class PackedGDN:
     def __init__(self, beta: torch.Tensor, gamma: torch.Tensor):
@@ -254,7 +302,7 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex).
     it: the row-tile count wp was packed with (0 = library default; explicit values go through ica_conv_ex)."""
     N, _, H, W, _ = x4.shape
-    if prec == PREC_BF16 or it:
+    if prec in (PREC_BF16, PREC_X6) or it:
         return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
     Wo = (W + 2 * (KS // 2) - KS) // S + 1
@@ -279,7 +327,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
             out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
-    if (prec == PREC_BF16 or it) and Cout != 3:
+    if (prec in (PREC_BF16, PREC_X6) or it) and Cout != 3:
         return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho, Wo = 2 * H, 2 * W
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)

@@ -67,6 +67,14 @@ int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, l
                               int flip, int it, hipStream_t stream);
 int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* beta_eff, int C, int transpose,
                       float beta_bound, hipStream_t stream);
+/* fp32-accurate bf16x6 packs for ica_conv_ex launches with prec = 2 (ica_conv_x6.hip; the anchors/utils.py:112-130
+ * k5 s2 conv / deconv layers of g_a and g_s and their input gradients).  Each weight w is split exactly into three
+ * bf16 parts w = hi + mid + lo; dst holds three planes (hi, mid, lo), each in the CC = 16 fragment order of
+ * ica_pack_conv_weight (order 0: conv_down, 1: conv_up) with row tiles it (> 0);
+ * ica_pack_conv_weight_x6_size(O, C, KS, it) bf16 values in all. */
+int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
+                            hipStream_t stream);
+size_t ica_pack_conv_weight_x6_size(int O, int C, int KS, int it);
 /* bf16 values ica_pack_conv_weight_bf16 writes.  C <= 4 (an RGB conv input; conv_down only) packs "tap groups":
  * k = 8h + j of MFMA tg is tap 4tg + 2h + (j>>2), channel j&3 (7 MFMAs per 32-row tile for 5x5 taps). */
 size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it);
@@ -162,7 +170,10 @@ typedef struct ica_conv_args {
   int N, Cin, Hin, Win, Cout, Hout, Wout;
   int kind, KS, S, epi, it, fill_mode, ps;
   int prec; /* 0: fp32 operands (exact fp32 MFMA); 1: bf16 operands, fp32 accumulate (wp / gp from the _bf16
-             * packers; bmshj2018 k5 s2 layers: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD) */
+             * packers; bmshj2018 k5 s2 layers: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD);
+             * 2: fp32-accurate bf16x6 operands (wp from ica_pack_conv_weight_x6, fp32 x / y / saved tensors and
+             * gp; k5 s2, Cin >= 16: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD, 128 output channels,
+             * or 96-multiples with the bias epilogue) */
 } ica_conv_args;
 int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);
 /* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
