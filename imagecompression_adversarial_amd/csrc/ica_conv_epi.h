@@ -50,12 +50,66 @@ struct ConvParams {
                       //    activations and epilogues, gp = the fp32 gamma' pack)
 };
 
+// v -> (hi, mid, lo) bf16 quads, each stage round-to-nearest-even on the residual (exact: hi + mid + lo == v)
+ICA_DEV void split3(f32x4 v, u32x2& hi, u32x2& mid, u32x2& lo) {
+  bf16x4 a, b, c;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    const float r1 = v[e] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    a[e] = h;
+    b[e] = m;
+    c[e] = (__bf16)r2;
+  }
+  hi = __builtin_bit_cast(u32x2, a);
+  mid = __builtin_bit_cast(u32x2, b);
+  lo = __builtin_bit_cast(u32x2, c);
+}
+
+// the six products of one 16-deep k step (small terms first)
+ICA_DEV f32x16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = mfma32bf(a[2], b[0], c);
+  c = mfma32bf(a[0], b[2], c);
+  c = mfma32bf(a[1], b[1], c);
+  c = mfma32bf(a[1], b[0], c);
+  c = mfma32bf(a[0], b[1], c);
+  c = mfma32bf(a[0], b[0], c);
+  return c;
+}
+
+// channels c0..c0+3 of a per-channel vector (bias, beta'): one 16-B buffer load, no branch.  A null vector gets a
+// zero-range descriptor and reads 0; the range is rounded up to whole quads (a quad that straddles C is read whole,
+// inside the allocation's 512-B granule) and callers mask channels >= Cout themselves.  (Element loads guarded by
+// p.bias / c < Cout compiled to one branch + s_waitcnt vmcnt(0) per element: serialised L2 round trips that made
+// the bias epilogue of a 1-wave/SIMD kernel cost ~20 us per block.)
+ICA_DEV __amdgpu_buffer_rsrc_t chan_rsrc(const float* v, int C) { return uniform_rsrc(v, v ? (unsigned)((C + 3) & ~3) * 4u : 0u); }
+ICA_DEV f32x4 ld_chan4(__amdgpu_buffer_rsrc_t r, int c0) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, c0 * 4, 0, 0));
+}
+
+// eight fp32 values (already in registers) -> the three bf16x8 planes of one MFMA operand
+ICA_DEV void split3x8(const float (&v)[8], bf16x8 (&o)[3]) {
+  u32x2 a0, b0, c0, a1, b1, c1;
+  split3(f32x4{v[0], v[1], v[2], v[3]}, a0, b0, c0);
+  split3(f32x4{v[4], v[5], v[6], v[7]}, a1, b1, c1);
+  o[0] = __builtin_bit_cast(bf16x8, u32x4_t{a0[0], a0[1], a1[0], a1[1]});
+  o[1] = __builtin_bit_cast(bf16x8, u32x4_t{b0[0], b0[1], b1[0], b1[1]});
+  o[2] = __builtin_bit_cast(bf16x8, u32x4_t{c0[0], c0[1], c1[0], c1[1]});
+}
+
 // --------------------------------------------------------------------------
 // Epilogue: acc[it] holds channels co_base + it*32 + acc_row(r,h) of pixel
 // (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
 // float4 of channel group c4 = co_base/4 + it*8 + 2g + h.
 // --------------------------------------------------------------------------
-template <int IT, int EPI, int FX, bool BF = false>
+// X6 (fp32 operands only): the GDN / IGDN normaliser GEMMs run as bf16x6 MFMAs on the split x^2 / t values and
+// the three-plane gamma' pack of ica_pack_gdn_x6 (p.gp).  X6 = 1 ("wide", for 1-wave/SIMD kernels with the whole
+// register file): all IT output tiles at once, gamma' fragments one round ahead; X6 = 2 ("narrow", for kernels
+// at 2 waves/SIMD, 256 registers): one output tile at a time, the other wave hides the fragment latency.
+// the three-plane gamma' pack of ica_pack_gdn_x6 (p.gp), fp32-accurate like the main loop of the x6 kernels.
+template <int IT, int EPI, int FX, bool BF = false, int X6 = 0>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
                            bool valid, int co_base) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -83,26 +137,22 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // (the shuffled tensor holds the same Cout * Hout * Wout floats per image as the plain one)
     const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n);
     const Img RS((FX & FX_RES) ? p.res : nullptr, img, n);
+    const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c0 = co_base + it * 32 + 8 * g + 4 * h;
-        if (c0 >= p.Cout) continue;
+        const f32x4 bv = ld_chan4(brs, c0);
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float t = acc[it][4 * g + e];
-          if (c0 + e < p.Cout) {
-            if (p.bias) t += p.bias[c0 + e];
-          } else {
-            t = 0.f;
-          }
+          float t = c0 + e < p.Cout ? acc[it][4 * g + e] + bv[e] : 0.f;
           if constexpr (EPI == EPI_RELU) t = fmaxf(t, 0.f);
           if constexpr (EPI == EPI_LRELU) t = t > 0.f ? t : t * 0.01f;
           v[e] = t;
         }
-        if (valid) {
+        if (valid && c0 < p.Cout) {
           unsigned vv, ss;
           if constexpr ((FX & FX_PS) != 0) {
             vv = vo_ps;
@@ -148,16 +198,58 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // n = beta' + gamma' x^2 at a time (16 accumulator registers live).
     const Img Y(p.y, img, n), SS(p.save_s, img, n);
     const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n), RS((FX & FX_RES) ? p.res : nullptr, img, n);
+    const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout), ers = chan_rsrc(p.beta, p.Cout);
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[it][r] += p.bias ? p.bias[it * 32 + acc_row(r, h)] : 0.f;
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bv = ld_chan4(brs, it * 32 + 8 * g + 4 * h);   // channels acc_row(4g + e, h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += bv[e];
+      }
     // bf16 path: x^2 (rounded to bf16) as the B operand of a bf16 GEMM with gamma' (its bf16 hi part; one
     // MFMA per k-step); the accumulator registers 8s..8s+7 of tile it are k-step s (pack_gdn_bf16_kernel gives
     // the matching gamma' order).  n = beta' + sum of non-negative terms then carries <= 2^-8 relative error,
     // s and y half of it: the size of the bf16 rounding of the stored y and s.
     bf16x8 xh[BF ? IT : 1][2];
-    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
+    // x6: every normaliser tile at once.  Round k = (k-tile it, k-step s) splits x^2 of accumulator registers
+    // 8s..8s+7 of tile it (fp32 square, exact 3-way split; the per-lane order of the fp32 gamma' pack that
+    // ica_pack_gdn_x6 splits, plane stride IT*IT*2048 bytes) and feeds all IT output tiles; the gamma' fragments
+    // of round k+1 are issued before round k's MFMAs (4 independent accumulation chains hide their latency).
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, X6 ? IT * IT * 6144 : IT * IT * 4096);
+    f32x16 nx[X6 == 1 ? IT : 1];
+    if constexpr (X6 == 1) {
+      static_assert(!BF, "x6 epilogue: fp32 activations");
+#pragma unroll
+      for (int ct = 0; ct < IT; ++ct)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) nx[ct][4 * g + e] = ev[e];
+        }
+      bf16x8 ga[2][IT][3];
+      auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
+#pragma unroll
+        for (int ct = 0; ct < IT; ++ct)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            a[ct][q] = ld_bf8(grs, lane * 16, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+      };
+      ldg(ga[0], 0);
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc[k >> 1][8 * (k & 1) + j] * acc[k >> 1][8 * (k & 1) + j];
+        bf16x8 xq[3];
+        split3x8(v, xq);
+#pragma unroll
+        for (int ct = 0; ct < IT; ++ct) nx[ct] = mfma_x6(ga[k & 1][ct], xq, nx[ct]);
+      }
+    }
     if constexpr (BF) {
 #pragma unroll
       for (int it = 0; it < IT; ++it)
@@ -172,10 +264,48 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
     for (int ct = 0; ct < IT; ++ct) {
       f32x16 nacc;
+      if constexpr (X6 == 1) {
+        nacc = nx[ct];
+      } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) nacc[r] = p.beta[ct * 32 + acc_row(r, h)];
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
+          for (int e = 0; e < 4; ++e) nacc[4 * g + e] = ev[e];
+        }
+      }
+      if constexpr (X6 == 2) {
+        // narrow x6: the output tile's gamma' fragments in two bursts of IT*3 (left to itself the scheduler loaded
+        // each next to its MFMA and waited out a full L2 round trip per fragment), x^2 split per k-step
+        static_assert(X6 != 2 || IT % 2 == 0, "narrow x6 epilogue: even IT");
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+          bf16x8 ga[IT / 2][2][3];
+#pragma unroll
+          for (int i2 = 0; i2 < IT / 2; ++i2)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+              for (int q = 0; q < 3; ++q)
+                ga[i2][s][q] = ld_bf8(grs, lane * 16,
+                                      ((ct * IT + hb * (IT / 2) + i2) * 2 + s) * 1024 + q * IT * IT * 2048);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i2 = 0; i2 < IT / 2; ++i2)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const int it = hb * (IT / 2) + i2;
+              float v[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = acc[it][8 * s + j] * acc[it][8 * s + j];
+              bf16x8 xq[3];
+              split3x8(v, xq);
+              nacc = mfma_x6(ga[i2][s], xq, nacc);
+            }
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < (X6 ? 0 : IT); ++it) {
         if constexpr (BF) {
           const int o = (ct * IT + it) * 4096;
 #pragma unroll
@@ -289,8 +419,10 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     } else if constexpr (FX == 0 && IT <= 4) {
       // fp32, plain layers: one pass over the saved (y, s) as well.  x = y / s, t and g*s are formed with the
       // ops of the two-pass form below and kept in registers (gs in place of g), so dx needs no second read.
-      f32x16 tt[IT], xx[IT];
+      f32x16 tt[X6 == 1 ? 1 : IT], xx[IT];
+      bf16x8 tq[X6 == 1 ? IT : 1][2][3];   // wide x6: t split into three planes (k-step s = registers 8s..8s+7)
       const unsigned vo_ld = valid ? vo : 0x0FFFFFF0u;  // past the descriptor's range: loads return 0
+      float tw[8];   // x6: t of register quads g = 2k, 2k+1 (one k-step) before the split
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int it = 0; it < IT; ++it)
@@ -302,39 +434,104 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           for (int e = 0; e < 4; ++e) {
             const float sg = sv[e], xs = yv[e] / sg;
             const float gx = acc[it][4 * g + e] * xs;
-            tt[it][4 * g + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
+            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
+            if constexpr (X6 == 1) tw[4 * (g & 1) + e] = tv;
+            else tt[it][4 * g + e] = tv;
             float gs = acc[it][4 * g + e] * sg;
             float x2 = 2.0f * xs;
             asm volatile("" : "+v"(gs), "+v"(x2));  // materialise (see the bf16 branch)
             acc[it][4 * g + e] = gs;
             xx[it][4 * g + e] = x2;
           }
+          if constexpr (X6 == 1) {
+            if (g & 1) split3x8(tw, tq[it][g >> 1]);
+          }
+          if constexpr (X6 == 2) {
+            // narrow x6 (256 registers): g*s parked in the output (same-thread write, re-read at the end) so the
+            // accumulator tiles are dead during the u GEMM
+            if (valid) Y.st(vo, ss, f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+          }
         }
       __builtin_amdgcn_sched_barrier(0);
+      // x6: u for every output tile at once; round k = (k-tile ct, k-step s) feeds all IT accumulators, the
+      // gamma'^T fragments of round k+1 issued before round k's MFMAs (as in the forward GDN epilogue)
+      f32x16 ux[X6 == 1 ? IT : 1];
+      bf16x8 gn[X6 == 2 ? IT / 2 : 1][2][3];   // narrow x6: half an output tile's gamma'^T fragments
+      if constexpr (X6 == 1) {
+        const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+#pragma unroll
+        for (int jt = 0; jt < IT; ++jt) ux[jt] = f32x16{0};
+        bf16x8 ga[2][IT][3];
+        auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
+#pragma unroll
+          for (int jt = 0; jt < IT; ++jt)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              a[jt][q] = ld_bf8(grs, lane * 16, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+        };
+        ldg(ga[0], 0);
+#pragma unroll
+        for (int k = 0; k < 2 * IT; ++k) {
+          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int jt = 0; jt < IT; ++jt) ux[jt] = mfma_x6(ga[k & 1][jt], tq[k >> 1][k & 1], ux[jt]);
+        }
+      }
 #pragma unroll
       for (int jt = 0; jt < IT; ++jt) {
         __builtin_amdgcn_sched_barrier(0);
         f32x16 uacc = f32x16{0};
 #pragma unroll
         for (int ct = 0; ct < IT; ++ct) {
-          const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
-          const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
-          const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
-                                g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+          if constexpr (X6 == 1) {
+            if (ct == 0) uacc = ux[jt];
+          } else if constexpr (X6 == 2) {
+            // narrow x6: the output tile's fragments in one burst at ct == 0 (see the forward epilogue), t of tile
+            // ct split per k-step on the fly (no 96-register three-plane copy)
+            if (ct % (IT / 2) == 0) {   // two bursts of IT*3 fragments per output tile
+              const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+              for (int c2 = 0; c2 < IT / 2; ++c2)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                  for (int q = 0; q < 3; ++q)
+                    gn[c2][s][q] = ld_bf8(grs, lane * 16, ((jt * IT + ct + c2) * 2 + s) * 1024 + q * IT * IT * 2048);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = tt[ct][8 * s + e];
+              bf16x8 tq2[3];
+              split3x8(v, tq2);
+              uacc = mfma_x6(gn[ct % (IT / 2)][s], tq2, uacc);
+            }
+          } else {
+            const float* gq = p.gp + ((size_t)(jt * IT + ct) * 64 + lane) * 16;
+            const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
+            const float ga[16] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3],
+                                  g2[0], g2[1], g2[2], g2[3], g3[0], g3[1], g3[2], g3[3]};
+#pragma unroll
+            for (int r = 0; r < 16; ++r) uacc = mfma32(ga[r], tt[ct][r], uacc);
+          }
         }
         if (valid) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             f32x4 v;
+            const f32x4 gs = X6 == 2 ? Y.ld(vo, so(jt * 8 + 2 * g)) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + xx[jt][4 * g + e] * uacc[4 * g + e];
+            for (int e = 0; e < 4; ++e)
+              v[e] = (X6 == 2 ? gs[e] : acc[jt][4 * g + e]) + xx[jt][4 * g + e] * uacc[4 * g + e];
             Y.st(vo, so(jt * 8 + 2 * g), v);
           }
         }
       }
     } else {
+      static_assert(!X6, "x6 GDN-bwd epilogue: plain layers, IT <= 4");
       if constexpr ((FX & FX_RES) != 0) {
         const Img SX(p.save_x, img, n), RS(p.res, img, n);
   #pragma unroll

@@ -12,7 +12,8 @@
 //
 // Storage stays fp32 (activations, saved tensors, gradients): the split happens when an input patch is staged into
 // LDS (three bf16 planes, 16-B entries of 8 channels) and, for the weights, once per weight version
-// (ica_pack_conv_weight_x6: three bf16 fragment planes).  The epilogues are the fp32 ones of ica_conv_epi.h.
+// (ica_pack_conv_weight_x6: three bf16 fragment planes).  The epilogues are the fp32 ones of ica_conv_epi.h, with
+// their GDN normaliser GEMMs on x6 operands as well (gamma' from ica_pack_gdn_x6).
 //
 //   conv_down_x6 : stride-2 5x5 conv.  Block = 4 waves x 2 pixel tiles x 32 px (8 x 32 outputs), IT x 32 output
 //                  channels; K loop = 16-channel LDS chunks x 25 taps, 6 x IT x 2 MFMAs per (chunk, tap).
@@ -24,37 +25,30 @@
 
 #include "ica_conv_epi.h"
 
+#ifdef ICA_X6_TRACE
+// phase timestamps (s_memtime cycles) per (block, wave): experiment builds only (scripts/exp/x6_trace.py)
+__device__ unsigned long long ica_x6_trace[32768 * 4 * 8];
+#define X6T(k)                                                                                                 \
+  do {                                                                                                         \
+    if ((threadIdx.x & 63) == 0) {                                                                             \
+      const unsigned b_ = blockIdx.x + gridDim.x * blockIdx.y;                                                 \
+      if (b_ < 32768) ica_x6_trace[((size_t)b_ * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_readcyclecounter(); \
+    }                                                                                                          \
+  } while (0)
+extern "C" int ica_x6_trace_read(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ica_x6_trace), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define X6T(k) \
+  do {         \
+  } while (0)
+#endif
+
 namespace {
 
-// v -> (hi, mid, lo) bf16 quads, each stage round-to-nearest-even on the residual (exact: hi + mid + lo == v)
-ICA_DEV void split3(f32x4 v, u32x2& hi, u32x2& mid, u32x2& lo) {
-  bf16x4 a, b, c;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const __bf16 h = (__bf16)v[e];
-    const float r1 = v[e] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    const float r2 = r1 - (float)m;
-    a[e] = h;
-    b[e] = m;
-    c[e] = (__bf16)r2;
-  }
-  hi = __builtin_bit_cast(u32x2, a);
-  mid = __builtin_bit_cast(u32x2, b);
-  lo = __builtin_bit_cast(u32x2, c);
-}
-
-// the six products of one 16-deep k step (small terms first)
-ICA_DEV f32x16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
-  c = mfma32bf(a[2], b[0], c);
-  c = mfma32bf(a[0], b[2], c);
-  c = mfma32bf(a[1], b[1], c);
-  c = mfma32bf(a[1], b[0], c);
-  c = mfma32bf(a[0], b[1], c);
-  c = mfma32bf(a[0], b[0], c);
-  return c;
-}
-
+#ifndef X6_PF
+#define X6_PF 1   // conv_down_x6 patch prefetch: 0 none, 1 first batch during the previous chunk, 2 both batches
+#endif
 constexpr int X6_PT = 2;                 // 32-pixel tiles per wave
 constexpr int XD_TW = 32, XD_TH = 4 * X6_PT;
 
@@ -117,16 +111,6 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
       }
     }
   };
-  auto fill = [&](int ch) {
-    f32x4 v[NB];
-    batch(ch, 0, v);
-    __syncthreads();
-    put(0, v);
-    batch(ch, NB, v);
-    put(NB, v);
-    __syncthreads();
-  };
-
   const int total = nch * KK;
   // weight fragments through one buffer descriptor: a per-lane byte offset and a wave-uniform (scalar) one
   const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
@@ -138,10 +122,12 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
 #pragma unroll
       for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
   };
-  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) {
-    const int ch = g / KK, tap = g - ch * KK;
-    if (tap == 0) fill(ch);
-    ldw(nxt, g + 1);  // one step ahead (ping-pong; a step is 6 x IT x PT MFMAs)
+  // one (chunk, tap) step: the next step's fragments are issued first, a whole step (48 MFMAs) ahead of their use
+  // (the barrier keeps the scheduler from sinking them to their first use); hook() issues patch loads after them
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g, int tap, auto hook) __attribute__((always_inline)) {
+    ldw(nxt, g + 1);
+    hook();
+    __builtin_amdgcn_sched_barrier(0);
     const int ky = tap / 5, kx = tap - ky * 5;
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
@@ -151,20 +137,155 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
       for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], b, acc[t][it]);
     }
   };
-  bf16x8 fa[IT][3], fb[IT][3];
-  ldw(fa, 0);
-  int g = 0;
+  auto none = []() {};
+  // the next chunk's patch is loaded into registers during the last KK - TPF taps of the current one (both
+  // batches, a straight-line tail so the waits stay exact) and staged into LDS between two barriers at the chunk
+  // boundary: only the split and the LDS writes remain exposed (the fill's HBM latency was ~30 % of the loop)
+#ifndef X6_TPF
+#define X6_TPF 20
+#endif
+  constexpr int TPF = X6_TPF;
+  f32x4 v1[NB], v2[NB];
+  auto chunk = [&](bf16x8 (&fa)[IT][3], bf16x8 (&fb)[IT][3], int ch) __attribute__((always_inline)) {
+    if constexpr (X6_PF < 0) batch(ch, 0, v1);
+    if constexpr (X6_PF == 1) batch(ch, NB, v2);
+    __syncthreads();
+    put(0, v1);
+    if constexpr (X6_PF <= 0) batch(ch, NB, v2);
+    put(NB, v2);
+    __syncthreads();
+    const int g0 = ch * KK, cn = min(ch + 1, nch - 1);
 #pragma unroll 1
-  for (; g + 1 < total; g += 2) {
-    step(fa, fb, g);
-    step(fb, fa, g + 1);
+    for (int tp = 0; tp < TPF; tp += 2) {
+      step(fa, fb, g0 + tp, tp, none);
+      step(fb, fa, g0 + tp + 1, tp + 1, none);
+    }
+    step(fa, fb, g0 + TPF, TPF, [&]() {
+      if constexpr (X6_PF >= 0) batch(cn, 0, v1);
+      if constexpr (X6_PF == 2) batch(cn, NB, v2);
+    });
+#pragma unroll
+    for (int tp = TPF + 1; tp < KK; ++tp) {
+      if ((tp - TPF) & 1) step(fb, fa, g0 + tp, tp, none);
+      else step(fa, fb, g0 + tp, tp, none);
+    }
+  };
+  static_assert(TPF % 2 == 0 && KK % 2 == 1, "chunk parity: a chunk starting on fa ends with the next fragments in fb");
+  X6T(0);
+  bf16x8 fa[IT][3], fb[IT][3];
+  if constexpr (X6_PF >= 0) batch(0, 0, v1);
+  if constexpr (X6_PF == 2) batch(0, NB, v2);
+  ldw(fa, 0);
+  int ch = 0;
+#pragma unroll 1
+  for (; ch + 1 < nch; ch += 2) {
+    chunk(fa, fb, ch);
+    chunk(fb, fa, ch + 1);
   }
-  if (g < total) step(fa, fb, g);
+  if (ch < nch) chunk(fa, fb, ch);
+  X6T(2);
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = oy0 + wave * PT + t, ox = ox0 + j;
-    conv_epilogue<IT, EPI, 0, false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+    conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
   }
+  X6T(3);
+}
+
+// --------------------------------------------------------------------------------------------------------------
+// conv_rgb_x6: the k5 s2 conv whose input is an RGB-sized map (Cin <= 4: g_a.0 forward, the g_s.6 input gradient)
+// as its PixelUnshuffle(2) view: a k3 s1 p1 conv over 16 virtual channels c' = 4 (2 sy + sx) + c at the output
+// resolution, x'[c'][u][v] = x[c][2u + sy][2v + sx]; the weight (ica_pack_conv_weight_x6 of w'[o][c'][ty][tx] =
+// w[o][c][2 ty + sy][2 tx + sx], zero where 2 ty + sy or 2 tx + sx is 5) covers the 5 x 5 taps with 3 x 3.  K is
+// 9 steps of 16 (vs 25 x 4 channels): the kernel is epilogue- and store-heavy, so it runs 2 blocks per CU with one
+// 32-pixel tile per wave, the fill / epilogue of one block overlapping the MFMAs of the other.
+// --------------------------------------------------------------------------------------------------------------
+#ifndef X6_RGB_BWD_WIDE
+#define X6_RGB_BWD_WIDE 1
+#endif
+// GDN-backward epilogue: t, 2x and g*s for all 128 channels plus the u GEMM do not fit 256 registers (the narrow
+// form spilled or stashed g*s in the output); it runs 1 block per CU with the wide epilogue
+template <int EPI>
+constexpr int rgb_x6_wide() { return (EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD) && X6_RGB_BWD_WIDE; }
+
+template <int IT, int EPI>
+__global__ __launch_bounds__(256, rgb_x6_wide<EPI>() ? 1 : 2) void conv_rgb_x6_kernel(ConvParams p, long ps) {
+  constexpr int KK = 9, TW = 32, TH = 4, PR = TH + 2, PC = TW + 2, PLANE = PR * PC;
+  constexpr int NF = (4 * PLANE + 255) / 256;
+  __shared__ f32x4 patch[3 * 2 * PLANE];   // [plane][half][pixel]: virtual channels 8h..8h+7 as bf16
+  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  X6T(0);
+  f32x16 acc[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+  // fill: entry e = (sub-pixel quad q, patch pixel) <- RGB quad of input pixel (2u + sy, 2v + sx); padding and
+  // pixels past the image read out of the descriptor's range (zeros); channel lane 3 is the nChw4c zero pad
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * p.Hin * p.Win * 16, (unsigned)p.Hin * p.Win * 16u);
+  f32x4 v[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+    const int iy = 2 * (oy0 - 1 + pr) + (q >> 1), ix = 2 * (ox0 - 1 + pc) + (q & 1);
+    const bool ok = e < 4 * PLANE && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+    const unsigned vo = ((unsigned)iy * p.Win + ix) * 16u;
+    v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+  }
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * KK * IT * 64;
+  auto ldw = [&](bf16x8 (&a)[IT][3], int g) {
+    const int f = wbase + g * IT * 64;
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+  };
+  bf16x8 fa[IT][3], fb[IT][3];
+  ldw(fa, 0);
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (e < 4 * PLANE) {
+      const int q = e / PLANE, pix = e - q * PLANE;
+      u32x2 a, b, c;
+      split3(v[i], a, b, c);
+      const int ent = (q >> 1) * PLANE + pix;
+      p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
+      p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+      p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+    }
+  }
+  __syncthreads();
+  X6T(1);
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) __attribute__((always_inline)) {
+    if (g + 1 < KK) ldw(nxt, g + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const int ky = g / 3, kx = g - 3 * (g / 3);
+    const int o = h * PLANE + (wave + ky) * PC + j + kx;
+    const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[it] = mfma_x6(cur[it], b, acc[it]);
+  };
+#pragma unroll
+  for (int g = 0; g < KK; ++g) {
+    if (g & 1) step(fb, fa, g);
+    else step(fa, fb, g);
+  }
+  X6T(2);
+  const int oy = oy0 + wave, ox = ox0 + j;
+  conv_epilogue<IT, EPI, 0, false, rgb_x6_wide<EPI>() ? 1 : 2>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout,
+                                                               cb * IT * 32);
+  X6T(3);
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -202,6 +323,9 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
   };
   auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int u) {
     ldw(nxt, u + 1);
+    // the next step's fragments are issued here, a whole step (48 MFMAs) ahead of their use: without the barrier
+    // the scheduler sank them next to their first use and waited on L2 latency every few MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     const int ti = u / NCG, c = u - ti * NCG;
     const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
     const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
@@ -281,7 +405,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
   const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
   // one class of the wave's pair: all channel groups (a group is re-staged per class when Cin > CG), then its
   // epilogue; classes pair 9 + 4 and 6 + 6 taps for balance
-  auto run_class = [&](auto py_c, auto px_c, bool refill) __attribute__((always_inline)) {
+  auto run_class = [&](auto py_c, auto px_c, bool refill, int tk) __attribute__((always_inline)) {
     constexpr int PY = decltype(py_c)::value, PX = decltype(px_c)::value;
     f32x16 acc[PT][IT];
 #pragma unroll
@@ -292,23 +416,31 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
       if (refill) fill(grp);
       conv_up_x6_class<PY, PX, IT, CG>(p, patch, jt, cb, nch, grp, ps, acc);
     }
+    X6T(tk);
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
+#ifdef ICA_X6_DENSE   // experiment: class-planar (dense) output addresses, wrong results
+      const int oy = PY * p.Hin + a0 + a_rel + 2 * t, ox = PX * p.Win + b0 + b_rel;
+#else
       const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-      conv_epilogue<IT, EPI, 0, false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+#endif
+      conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
     }
+    X6T(tk + 1);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   const bool multi = ngrp > 1;
+  X6T(0);
   if (!multi) fill(0);
+  X6T(1);
   // every wave joins every fill barrier: both classes of every wave run the same group sequence
   if (wave < 2) {
-    run_class(I0{}, I0{}, multi);
-    run_class(I1{}, I1{}, multi);
+    run_class(I0{}, I0{}, multi, 2);
+    run_class(I1{}, I1{}, multi, 4);
   } else {
-    run_class(I0{}, I1{}, multi);
-    run_class(I1{}, I0{}, multi);
+    run_class(I0{}, I1{}, multi, 2);
+    run_class(I1{}, I0{}, multi, 4);
   }
 }
 
@@ -341,12 +473,38 @@ __global__ void pack_conv_x6_kernel(const float* __restrict__ w, __bf16* __restr
   dst[2 * total + i] = (__bf16)(r1 - (float)b);
 }
 
+// the fp32 gamma' pack of ica_pack_gdn ([a][b][lane][r]) -> three bf16 planes [plane][a][b][s][lane][e], r = 8s + e
+// (the epilogue's k-step s of tile b, lane order unchanged)
+__global__ void pack_gdn_x6_kernel(const float* __restrict__ gp, __bf16* __restrict__ dst, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int e = i % 8, lane = (i / 8) % 64, s = (i / 512) % 2;
+  const long ab = i / 1024;
+  const float v = gp[(ab * 64 + lane) * 16 + 8 * s + e];
+  const __bf16 a = (__bf16)v;
+  const float r1 = v - (float)a;
+  const __bf16 b = (__bf16)r1;
+  dst[i] = a;
+  dst[total + i] = b;
+  dst[2 * total + i] = (__bf16)(r1 - (float)b);
+}
+
 template <int IT, int EPI>
 int launch_down_x6(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + XD_TH - 1) / XD_TH) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * ((((p.Cin + 3) / 4) * 4 + 15) / 16) * 25 * IT * 64;
   hipLaunchKernelGGL((conv_down_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int IT, int EPI>
+int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Wout + 31) / 32) * ((p.Hout + 3) / 4) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * 9 * IT * 64;
+  hipLaunchKernelGGL((conv_rgb_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -388,7 +546,17 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
   if (KS != 5 || S != 2 || fx != 0) return -4;
   if (p.Cout % 32 != 0) return -4;
   if (kind == 0) {
-    if (p.Cin < 16 || p.Hout * 2 != p.Hin + (p.Hin & 1) || p.Wout * 2 != p.Win + (p.Win & 1)) return -2;
+    if (p.Hout * 2 != p.Hin + (p.Hin & 1) || p.Wout * 2 != p.Win + (p.Win & 1)) return -2;
+    if (p.Cin <= 4) {   // RGB-sized input: the PixelUnshuffle(2) k3 view (wp from the rearranged weight)
+      if (it != 4) return -3;
+      switch (epi) {
+        case EPI_BIAS: return launch_rgb_x6<4, EPI_BIAS>(p, st);
+        case EPI_GDN: return launch_rgb_x6<4, EPI_GDN>(p, st);
+        case EPI_IGDN_BWD: return launch_rgb_x6<4, EPI_IGDN_BWD>(p, st);
+        default: return -5;
+      }
+    }
+    if (p.Cin < 16) return -2;
     if (it == 4) {
       switch (epi) {
         case EPI_BIAS: return launch_down_x6<4, EPI_BIAS>(p, st);
@@ -421,6 +589,18 @@ size_t ica_pack_conv_weight_x6_size(int O, int C, int KS, int IT) {
   const int ncb = (O + IT * 32 - 1) / (IT * 32);
   const int nch = (((C + 3) / 4) * 4 + 15) / 16;
   return (size_t)3 * ncb * nch * KS * KS * IT * 64 * 8;
+}
+
+size_t ica_pack_gdn_x6_size(int C) { return (size_t)3 * (C / 32) * (C / 32) * 2048; }
+
+// three bf16 planes of an fp32 gamma' / gamma'^T pack (ica_pack_gdn output) for the x6 GDN epilogues
+int ica_pack_gdn_x6(const float* gp, void* dst, int C, hipStream_t st) {
+  if (C % 32 != 0) return -2;
+  const long total = (long)(C / 32) * (C / 32) * 1024;
+  hipLaunchKernelGGL(pack_gdn_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gp,
+                     reinterpret_cast<__bf16*>(dst), total);
+  ICA_CHECK_LAUNCH();
+  return 0;
 }
 
 // three bf16 planes (hi, mid, lo) of the 16-channel-chunk fragment pack; order 0: conv_down [cb][chunk][tap],

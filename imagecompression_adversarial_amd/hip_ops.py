@@ -142,6 +142,16 @@ def pack_conv_x6(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, or
     return dst
 
 
+def rgb_unshuffle_weight(w: torch.Tensor) -> torch.Tensor:
+    """k5 s2 weight [O][C <= 4][5][5] of a conv whose input is an RGB-sized map -> the k3 weight [O][16][3][3] of
+    its PixelUnshuffle(2) view (conv_rgb_x6_kernel): w'[o][4 (2 sy + sx) + c][ty][tx] = w[o][c][2 ty + sy][2 tx + sx],
+    zero where a tap index reaches 5."""
+    O, C = w.shape[0], w.shape[1]
+    wp = torch.zeros(O, 4, 6, 6, dtype=w.dtype, device=w.device)
+    wp[:, :C, :5, :5] = w.detach()
+    return wp.view(O, 4, 3, 2, 3, 2).permute(0, 3, 5, 1, 2, 4).reshape(O, 16, 3, 3).contiguous()
+
+
 def x6_ok(O: int, C: int, it: int) -> bool:
     """Layers the x6 kernels cover: k5 s2, >= 16 input channels, 128 output channels (IT 4, every epilogue) or
     96-multiples at IT 3 (bias), no explicit 6-tile (C = 192 GDN) launch."""
@@ -239,15 +249,21 @@ class PackedConv:
         self.bias = None if bias is None else bias.detach().contiguous()
 
     def _init_x6(self, weight, bias, kind, stride):
-        """PREC_X6: the k5 s2 launches with >= 16 channels on both ends run on the bf16x6 kernels; the RGB ends
-        (3-channel conv input / transposed-conv output) and explicit 6-tile layers keep the fp32 packs."""
+        """PREC_X6: the k5 s2 launches run on the bf16x6 kernels: >= 16 channels on both ends (conv_down_x6 /
+        conv_up_x6) and the conv_downs whose input is RGB-sized (g_a.0 forward, g_s.6 input gradient: conv_rgb_x6 on
+        the PixelUnshuffle(2) view).  The 3-channel transposed-conv outputs (conv_up3) and explicit 6-tile layers
+        keep the fp32 packs."""
         fp = PackedConv(weight, bias, kind, stride, PREC_FP32, self.it_fwd, self.it_bwd)
         self.__dict__.update(fp.__dict__)
         if self.KS != 5 or stride != 2:
             return
         KK = 25
+        rgb_ok = lambda O, it: it == 0 and x6_it(O) == 4   # noqa: E731  (conv_rgb_x6: IT 4 launches)
         if kind == "conv":
-            if x6_ok(self.Cout, self.Cin, self.it_fwd):     # forward conv_down: o = co, c = ci
+            if self.Cin <= 4 and rgb_ok(self.Cout, self.it_fwd):   # forward from the RGB image: unshuffled k3 view
+                self.fwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cout, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
+                self.fwd_prec = PREC_X6
+            elif x6_ok(self.Cout, self.Cin, self.it_fwd):     # forward conv_down: o = co, c = ci
                 self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN, x6_it(self.Cout))
                 self.fwd_prec = PREC_X6
             if self.Cin != 3 and x6_ok(self.Cin, self.Cout, self.it_bwd):   # dgrad conv_up: o = ci, c = co
@@ -257,7 +273,10 @@ class PackedConv:
             if self.Cout != 3 and x6_ok(self.Cout, self.Cin, self.it_fwd):  # forward conv_up: o = co, c = ci
                 self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP, x6_it(self.Cout))
                 self.fwd_prec = PREC_X6
-            if x6_ok(self.Cin, self.Cout, self.it_bwd):       # dgrad conv_down: o = ci, c = co
+            if self.Cout <= 4 and rgb_ok(self.Cin, self.it_bwd):   # dgrad from the RGB-sized gradient (view [ci][co])
+                self.bwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cin, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
+                self.bwd_prec = PREC_X6
+            elif x6_ok(self.Cin, self.Cout, self.it_bwd):       # dgrad conv_down: o = ci, c = co
                 self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, x6_it(self.Cin))
                 self.bwd_prec = PREC_X6
 
@@ -277,6 +296,17 @@ class PackedGDN:
         call("ica_pack_gdn", ptr(gamma), ptr(beta), ptr(self.gpT), ptr(self.beta), C, 1, GDN_BETA_BOUND, stream())
         self._src = (gamma, beta)
         self.gpb = self.gpbT = None
+        self.gpx = self.gpxT = None
+
+    def x6(self):
+        """Three-plane bf16 splits of gamma' / gamma'^T for prec=2 epilogues (built once, on first use)."""
+        if self.gpx is None:
+            n = int(lib().ica_pack_gdn_x6_size(self.C))
+            self.gpx = torch.empty(n // 2, dtype=torch.bfloat16, device=self.gp.device)
+            self.gpxT = torch.empty_like(self.gpx)
+            call("ica_pack_gdn_x6", ptr(self.gp), ptr(self.gpx), self.C, stream())
+            call("ica_pack_gdn_x6", ptr(self.gpT), ptr(self.gpxT), self.C, stream())
+        return self
 
     def bf16(self):
         """bf16x3 hi/lo fragments of gamma' / gamma'^T for prec=1 epilogues (built once, on first use)."""
@@ -399,6 +429,9 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
         if prec == PREC_BF16:
             gdn.bf16()
             gp = gdn.gpbT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpb
+        elif prec == PREC_X6:
+            gdn.x6()
+            gp = gdn.gpxT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpx
         else:
             gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
     a = ConvArgs(ptr(x4), ptr(y), ptr(wp), ptr(bias), ptr(gp), ptr(None if gdn is None else gdn.beta), ptr(save_x),

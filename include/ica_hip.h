@@ -75,6 +75,10 @@ int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* b
 int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
                             hipStream_t stream);
 size_t ica_pack_conv_weight_x6_size(int O, int C, int KS, int it);
+/* The fp32 gamma' (or gamma'^T) pack of ica_pack_gdn split exactly into three bf16 planes for the x6 GDN / IGDN
+ * epilogues (their normaliser GEMMs run as bf16x6 MFMAs too); ica_pack_gdn_x6_size(C) bytes. */
+int ica_pack_gdn_x6(const float* gp, void* dst, int C, hipStream_t stream);
+size_t ica_pack_gdn_x6_size(int C);
 /* bf16 values ica_pack_conv_weight_bf16 writes.  C <= 4 (an RGB conv input; conv_down only) packs "tap groups":
  * k = 8h + j of MFMA tg is tap 4tg + 2h + (j>>2), channel j&3 (7 MFMAs per 32-row tile for 5x5 taps). */
 size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it);
@@ -171,8 +175,8 @@ typedef struct ica_conv_args {
   int kind, KS, S, epi, it, fill_mode, ps;
   int prec; /* 0: fp32 operands (exact fp32 MFMA); 1: bf16 operands, fp32 accumulate (wp / gp from the _bf16
              * packers; bmshj2018 k5 s2 layers: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD);
-             * 2: fp32-accurate bf16x6 operands (wp from ica_pack_conv_weight_x6, fp32 x / y / saved tensors and
-             * gp; k5 s2, Cin >= 16: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD, 128 output channels,
+             * 2: fp32-accurate bf16x6 operands (wp from ica_pack_conv_weight_x6, gp from ica_pack_gdn_x6, fp32
+             * x / y / saved tensors; k5 s2, Cin >= 16: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD, 128 output channels,
              * or 96-multiples with the bias epilogue) */
 } ica_conv_args;
 int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);

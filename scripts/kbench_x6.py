@@ -43,6 +43,18 @@ for pr, nm in ((K.PREC_FP32, "fp32"), (K.PREC_X6, "x6")):
         f"{nm} up.gdn_bwd": lambda wc=wc: K.conv_up(x_lo, N, wc.bwd, None, N, K.EPI_GDN_BWD, gd, saved=(sx_hi, ss_hi),
                                                   prec=wc.bwd_prec),
     })
+W3 = r(N, 3, 5, 5) * 0.1
+R = {pr: (K.PackedConv(W3, b, "conv", 2, pr), K.PackedConv(W3, None, "deconv", 2, pr)) for pr in (K.PREC_FP32, K.PREC_X6)}
+x_rgb = K.empty_nc4(B, 3, 512, 768, dev).uniform_(0, 1)
+flop_rgb = 2 * N * 3 * 25 * 256 * 384 * B
+for pr, nm in ((K.PREC_FP32, "fp32"), (K.PREC_X6, "x6")):
+    rc, rd = R[pr]
+    cases.update({
+        f"{nm} rgb.gdn(save)": lambda rc=rc: K.conv_down(x_rgb, 3, rc.fwd, rc.bias, N, 5, 2, K.EPI_GDN, gd, save=True,
+                                                       prec=rc.fwd_prec),
+        f"{nm} rgb.igdn_bwd": lambda rd=rd: K.conv_down(x_rgb, 3, rd.bwd, None, N, 5, 2, K.EPI_IGDN_BWD, gd,
+                                                      saved=(sx_hi, ss_hi), prec=rd.bwd_prec),
+    })
 cases = {k: f for k, f in cases.items() if only in k}
 times = {k: [] for k in cases}
 for rnd in range(6):
@@ -57,4 +69,5 @@ for rnd in range(6):
         del out
 for k, v in times.items():
     ms = statistics.median(v)
-    print(f"{k:22s} {ms:7.3f} ms  {flop / ms / 1e9:7.1f} TFLOP/s (conv only)", flush=True)
+    fl = flop_rgb if "rgb" in k else flop
+    print(f"{k:22s} {ms:7.3f} ms  {fl / ms / 1e9:7.1f} TFLOP/s (conv only)", flush=True)
