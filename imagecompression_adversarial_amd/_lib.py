@@ -34,6 +34,8 @@ _SIGS = {
     "ica_pack_gdn_x6": [_p, _p, _i, _p],
     "ica_pack_gdn_x6_size": [_i],
     "ica_pack_up3_bf16": [_p, _p, _i, _p],
+    "ica_pack_up3_x6": [_p, _p, _i, _p],
+    "ica_conv_up3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
     "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],

@@ -697,7 +697,10 @@ constexpr int T3_ROWS = 75, T3_JT = (T3_NPX + 31) / 32;                         
 constexpr int T3_NCH_BF = 8;  // bf16 up-front-load path: Cin = 128
 constexpr int T3_BLOCKS = (2 * T3_ROWS * T3_NPX * 4 <= 160 * 1024) ? 2 : 1;
 
-template <bool BF>
+// X6: fp32-accurate bf16x6 operands (weights from pack_up3_x6_kernel: three planes [plane][it][chunk][lane][8];
+// activations split per chunk in registers), six 32x32x16 MFMAs per 16-channel chunk and row tile instead of
+// eight 32x32x2 fp32 ones per 2 channels: the fp32 Z GEMM is MFMA-bound (~1 ms of the 1.3 ms kernel at 512x768)
+template <bool BF, bool X6 = false>
 __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) {
   __shared__ float zs[T3_ROWS * T3_NPX];
   const int tiles_x = (p.Win + T3_TW - 1) / T3_TW, tiles_y = (p.Hin + T3_TH - 1) / T3_TH;
@@ -812,6 +815,42 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
           }
         }
       }
+    } else if constexpr (X6) {
+      const long pst = 3L * nch * 64;   // fragments per plane
+      const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * pst * 16));
+      const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
+      const unsigned po = ok ? (unsigned)(iy * p.Win + ix) * 16u : 0xFFFFFFF0u;
+      auto load = [&](int ch, bf16x8 (&a)[3][3], f32x4& v0, f32x4& v1) {
+#pragma unroll
+        for (int it = 0; it < 3; ++it)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * pst + ((long)it * nch + ch) * 64) * 16));
+        const unsigned o0 = ok ? po + (unsigned)((4 * ch + 2 * h) * plane) * 16u : 0xFFFFFFF0u;
+        v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o0, 0, 0));
+        v1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? o0 + (unsigned)plane * 16u
+                                                                                     : 0xFFFFFFF0u, 0, 0));
+      };
+      auto compute = [&](const bf16x8 (&a)[3][3], const f32x4& v0, const f32x4& v1) {
+        const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        bf16x8 b[3];
+        split3x8(v, b);
+#pragma unroll
+        for (int it = 0; it < 3; ++it) acc[it] = mfma_x6(a[it], b, acc[it]);
+      };
+      bf16x8 aa[3][3], ab[3][3];
+      f32x4 xa0, xa1, xb0, xb1;
+      load(0, aa, xa0, xa1);
+      int ch = 0;
+#pragma unroll 1
+      for (; ch + 1 < nch; ch += 2) {
+        load(ch + 1, ab, xb0, xb1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(aa, xa0, xa1);
+        load(min(ch + 2, nch - 1), aa, xa0, xa1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(ab, xb0, xb1);
+      }
+      if (ch < nch) compute(aa, xa0, xa1);
     } else {
       const float* wl = p.wp + (size_t)lane * 8;
       // B (activations, straight from HBM: 32 consecutive pixels x 16 B per plane = 512 B
@@ -893,6 +932,27 @@ gather:
         st4(p.y + (((size_t)n * p.Hout + y) * p.Wout + x) * 4, f32x4{o0 + bias0, o1 + bias1, o2 + bias2, 0.f});
     }
   }
+}
+
+// x6 weights for conv_up3: the pack_up3_kernel fragment order, each value split exactly into three bf16 planes
+__global__ void pack_up3_x6_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int Cin, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int nch = Cin / 16;
+  long t = i;
+  const int s = t % 8; t /= 8;
+  const int lane = t % 64; t /= 64;
+  const int ch = t % nch; t /= nch;
+  const int row = (int)t * 32 + (lane & 31);
+  const int c = ch * 16 + (lane >> 5) * 8 + s;
+  float v = 0.f;
+  if (row < T3_ROWS) v = w[((size_t)c * 3 + row / 25) * 25 + row % 25];
+  const __bf16 a = (__bf16)v;
+  const float r1 = v - (float)a;
+  const __bf16 b = (__bf16)r1;
+  dst[i] = a;
+  dst[total + i] = b;
+  dst[2 * total + i] = (__bf16)(r1 - (float)b);
 }
 
 template <typename T>
@@ -1344,6 +1404,28 @@ int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, i
                2 * Hin, 2 * Win, nullptr};
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
   hipLaunchKernelGGL(conv_up3_kernel<false>, dim3(tiles), dim3(256), 0, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp32-accurate bf16x6 variants (prec = 2): three bf16 planes of the fp32 fragment order (3 * ica_pack_up3_size(Cin)
+// values)
+int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t st) {
+  if (Cin % 16 != 0) return -2;
+  const long total = (long)ica_pack_up3_size(Cin);
+  hipLaunchKernelGGL(pack_up3_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
+                     reinterpret_cast<__bf16*>(dst), Cin, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                    hipStream_t st) {
+  if (Cin % 16 != 0) return -2;
+  ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+               N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
+  const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
+  hipLaunchKernelGGL((conv_up3_kernel<false, true>), dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }

@@ -163,12 +163,15 @@ def conv_cc(Cin: int) -> int:
 
 
 def pack_up3(w_view: torch.Tensor, prec: int = 0) -> torch.Tensor:
-    """Fragments for conv_up3 from a [Cin][3][5][5] transposed-conv weight view (prec 1: bf16)."""
+    """Fragments for conv_up3 from a [Cin][3][5][5] transposed-conv weight view (prec 1: bf16, 2: x6)."""
     w = w_view.detach().contiguous()
     _dev_check(w, "weight")
     Cin = w.shape[0]
     n = int(lib().ica_pack_up3_size(Cin))
-    if prec:
+    if prec == PREC_X6:
+        dst = torch.empty(3 * n, dtype=torch.bfloat16, device=w.device)
+        call("ica_pack_up3_x6", ptr(w), ptr(dst), Cin, stream())
+    elif prec:
         dst = torch.empty(n, dtype=torch.bfloat16, device=w.device)
         call("ica_pack_up3_bf16", ptr(w), ptr(dst), Cin, stream())
     else:
@@ -251,7 +254,7 @@ class PackedConv:
     def _init_x6(self, weight, bias, kind, stride):
         """PREC_X6: the k5 s2 launches run on the bf16x6 kernels: >= 16 channels on both ends (conv_down_x6 /
         conv_up_x6) and the conv_downs whose input is RGB-sized (g_a.0 forward, g_s.6 input gradient: conv_rgb_x6 on
-        the PixelUnshuffle(2) view).  The 3-channel transposed-conv outputs (conv_up3) and explicit 6-tile layers
+        the PixelUnshuffle(2) view) and the 3-channel transposed-conv outputs (x6 conv_up3).  Explicit 6-tile layers
         keep the fp32 packs."""
         fp = PackedConv(weight, bias, kind, stride, PREC_FP32, self.it_fwd, self.it_bwd)
         self.__dict__.update(fp.__dict__)
@@ -259,6 +262,12 @@ class PackedConv:
             return
         KK = 25
         rgb_ok = lambda O, it: it == 0 and x6_it(O) == 4   # noqa: E731  (conv_rgb_x6: IT 4 launches)
+        if kind == "conv" and self.Cin == 3 and self.Cout % 16 == 0:    # input gradient to RGB: x6 conv_up3
+            self.bwd = pack_up3(weight, PREC_X6)
+            self.bwd_prec = PREC_X6
+        if kind == "deconv" and self.Cout == 3 and self.Cin % 16 == 0:  # g_s.6 forward to RGB: x6 conv_up3
+            self.fwd = pack_up3(weight, PREC_X6)
+            self.fwd_prec = PREC_X6
         if kind == "conv":
             if self.Cin <= 4 and rgb_ok(self.Cout, self.it_fwd):   # forward from the RGB image: unshuffled k3 view
                 self.fwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cout, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
@@ -365,7 +374,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
         if epi != EPI_BIAS:
             raise RuntimeError("conv_up to 3 channels supports the bias epilogue only")
         ev = _ev_begin(tag, N)
-        call("ica_conv_up3_bf16" if prec == PREC_BF16 else "ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
+        call({PREC_BF16: "ica_conv_up3_bf16", PREC_X6: "ica_conv_up3_x6"}.get(prec, "ica_conv_up3"), ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
              Cin, H, W, stream())
         _ev_end(ev)
         return y, None, None

@@ -83,6 +83,11 @@ size_t ica_pack_gdn_x6_size(int C);
  * k = 8h + j of MFMA tg is tap 4tg + 2h + (j>>2), channel j&3 (7 MFMAs per 32-row tile for 5x5 taps). */
 size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it);
 /* bf16 Z-gather transposed conv to 3 channels (g_s last layer / g_a first-layer input-gradient). */
+/* fp32-accurate bf16x6 conv_up3 (prec 2): three bf16 planes of the ica_pack_up3 fragment order
+ * (3 * ica_pack_up3_size(Cin) values); same semantics and argument meaning as ica_conv_up3. */
+int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t stream);
+int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
+                    hipStream_t stream);
 int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t stream);
 int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
                       hipStream_t stream);

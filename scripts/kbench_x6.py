@@ -55,6 +55,9 @@ for pr, nm in ((K.PREC_FP32, "fp32"), (K.PREC_X6, "x6")):
         f"{nm} rgb.igdn_bwd": lambda rd=rd: K.conv_down(x_rgb, 3, rd.bwd, None, N, 5, 2, K.EPI_IGDN_BWD, gd,
                                                       saved=(sx_hi, ss_hi), prec=rd.bwd_prec),
     })
+U3 = {pr: K.PackedConv(W3, b[:3].contiguous(), "deconv", 2, pr) for pr in (K.PREC_FP32, K.PREC_X6)}
+for pr, nm in ((K.PREC_FP32, "fp32"), (K.PREC_X6, "x6")):
+    cases[f"{nm} up3.bias"] = lambda u=U3[pr]: K.conv_up(x_hi, N, u.fwd, u.bias, 3, K.EPI_BIAS, prec=u.fwd_prec)
 cases = {k: f for k, f in cases.items() if only in k}
 times = {k: [] for k in cases}
 for rnd in range(6):
@@ -69,5 +72,5 @@ for rnd in range(6):
         del out
 for k, v in times.items():
     ms = statistics.median(v)
-    fl = flop_rgb if "rgb" in k else flop
+    fl = flop_rgb if ("rgb" in k or "up3" in k) else flop
     print(f"{k:22s} {ms:7.3f} ms  {fl / ms / 1e9:7.1f} TFLOP/s (conv only)", flush=True)
