@@ -331,7 +331,9 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
             const float nv = nacc[4 * g + e];
             // bf16 path: v_rsq_f32 / v_sqrt_f32 (1 ulp; n >= beta' > 0), no IEEE division / sqrt fix-ups
             float s;
-            if constexpr (BF) s = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+            // x6: the same 1-ulp instructions (1/sqrtf rounds twice, so the IEEE form is no closer; measured
+            // 8-10k cycles per conv_up class of IEEE sqrt fix-ups)
+            if constexpr (BF || X6) s = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
             else s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
             sv[e] = s;
             yv[e] = acc[ct][4 * g + e] * s;
@@ -661,3 +663,80 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
   }
 }
 
+// --------------------------------------------------------------------------
+// GDN / IGDN forward epilogue of TWO pixel tiles of one wave (the x6 kernels' PT = 2), fp32 activations, x6
+// normaliser GEMM: every gamma' fragment round feeds both tiles (2 x IT x 6 MFMAs per 3 x IT fragment loads, the
+// next round's loads a whole round = 1.5k cycles ahead), which halves the fragment traffic of two single-tile
+// epilogues and hides its L2 latency.  Requires IT*32 == Cout, co_base == 0, FX == 0.
+// --------------------------------------------------------------------------
+template <int IT, int EPI>
+ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, const int (&oy)[2],
+                             const int (&ox)[2]) {
+  static_assert(EPI == EPI_GDN || EPI == EPI_IGDN, "forward GDN epilogues only");
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int C4o = (p.Cout + 3) >> 2;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)C4o * plane;
+  const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+  const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout), ers = chan_rsrc(p.beta, p.Cout);
+  const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+  f32x16 nx[2][IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = ld_chan4(brs, it * 32 + 8 * g + 4 * h), ev = ld_chan4(ers, it * 32 + 8 * g + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[0][it][4 * g + e] += bv[e];
+        acc[1][it][4 * g + e] += bv[e];
+        nx[0][it][4 * g + e] = ev[e];
+        nx[1][it][4 * g + e] = ev[e];
+      }
+    }
+  bf16x8 ga[2][IT][3];
+  auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
+#pragma unroll
+    for (int ct = 0; ct < IT; ++ct)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        a[ct][q] = ld_bf8(grs, lane * 16, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+  };
+  ldg(ga[0], 0);
+#pragma unroll
+  for (int k = 0; k < 2 * IT; ++k) {
+    if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = acc[t][k >> 1][8 * (k & 1) + j] * acc[t][k >> 1][8 * (k & 1) + j];
+      bf16x8 xq[3];
+      split3x8(v, xq);
+#pragma unroll
+      for (int ct = 0; ct < IT; ++ct) nx[t][ct] = mfma_x6(ga[k & 1][ct], xq, nx[t][ct]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (oy[t] >= p.Hout || ox[t] >= p.Wout) continue;
+    const unsigned vo = h * plane + (unsigned)oy[t] * p.Wout + ox[t];
+#pragma unroll
+    for (int ct = 0; ct < IT; ++ct)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 yv, sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float nv = nx[t][ct][4 * g + e];
+          const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+          sv[e] = sc;
+          yv[e] = acc[t][ct][4 * g + e] * sc;
+        }
+        const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
+        if (p.save_s) SS.st(vo, ss, sv);
+        Y.st(vo, ss, yv);
+      }
+  }
+}

@@ -184,10 +184,15 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
   }
   if (ch < nch) chunk(fa, fb, ch);
   X6T(2);
+  if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
+    const int oy[2] = {oy0 + wave * PT, oy0 + wave * PT + 1}, ox[2] = {ox0 + j, ox0 + j};
+    gdn_fwd_x6_pair<IT, EPI>(p, acc, n, oy, ox);
+  } else {
 #pragma unroll
-  for (int t = 0; t < PT; ++t) {
-    const int oy = oy0 + wave * PT + t, ox = ox0 + j;
-    conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+    for (int t = 0; t < PT; ++t) {
+      const int oy = oy0 + wave * PT + t, ox = ox0 + j;
+      conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+    }
   }
   X6T(3);
 }
@@ -417,14 +422,16 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
       conv_up_x6_class<PY, PX, IT, CG>(p, patch, jt, cb, nch, grp, ps, acc);
     }
     X6T(tk);
+    if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
+      const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
+      const int ox[2] = {2 * (b0 + b_rel) + PX, 2 * (b0 + b_rel) + PX};
+      gdn_fwd_x6_pair<IT, EPI>(p, acc, n, oy, ox);
+    } else {
 #pragma unroll
-    for (int t = 0; t < PT; ++t) {
-#ifdef ICA_X6_DENSE   // experiment: class-planar (dense) output addresses, wrong results
-      const int oy = PY * p.Hin + a0 + a_rel + 2 * t, ox = PX * p.Win + b0 + b_rel;
-#else
-      const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-#endif
-      conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+      for (int t = 0; t < PT; ++t) {
+        const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
+        conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+      }
     }
     X6T(tk + 1);
   };
