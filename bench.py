@@ -268,8 +268,8 @@ def main():
     ap.add_argument("--quality", type=int, default=None, help="default 3 (hyper) / 6 (cheng2020)")
     ap.add_argument("--model", default="hyper", choices=("hyper", "cheng2020"))
     ap.add_argument("--precision", default=None, choices=("fp32", "x6", "bf16"),
-                    help="conv operand precision of g_a/g_s: fp32 (fp32-operand MFMA), x6 (fp32-accurate bf16x6 "
-                         "split-operand MFMA), bf16 (config 5 default)")
+                    help="conv operand precision of g_a/g_s: x6 (default: fp32-accurate bf16x6 split-operand "
+                         "MFMA), fp32 (fp32-operand MFMA; cheng2020 default), bf16 (config 5 default)")
     ap.add_argument("--config", type=int, default=None, choices=(2, 3, 4, 5),
                     help="BASELINE.json configs[k-1] per-GPU shard: 2 hyper q3 fp32 (default), 3 cheng2020 q6, "
                          "4 train.py --adv fine-tune outer steps (8 x 256^2 per GPU, 300 inner steps, RCCL grad "
@@ -295,8 +295,8 @@ def main():
             args.batch = 8
         if args.precision is None:
             args.precision = "bf16"
-    if args.precision is None:
-        args.precision = "fp32"
+    if args.precision is None:   # the attack engine's default: x6 (fp32-accurate) for bmshj2018, fp32 for cheng2020
+        args.precision = "x6" if args.model == "hyper" else "fp32"
     if args.precision == "bf16" and args.model != "hyper":
         raise SystemExit("the bf16 conv path covers the bmshj2018 transforms (config 5)")
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -51,7 +51,7 @@ def attack_(im_s, net, args):
     For B > 1 the metric dicts hold lists (one entry per image)."""
     if getattr(args, "defend", False):
         raise NotImplementedError("--defend is not supported (it crashes inside the reference step loop)")
-    kern = net.kernels(getattr(args, "precision", "fp32"))
+    kern = net.kernels(net.attack_precision(getattr(args, "precision", None)))
     init_noise = None
     if args.random > 1:
         init_noise = torch.empty_like(im_s).uniform_(-1e-2, 1e-2)

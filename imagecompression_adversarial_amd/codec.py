@@ -648,6 +648,13 @@ class CompressionModel(nn.Module):
                 updated |= m.update_scale_table(scale_table, force=force)
         return updated
 
+    def attack_precision(self, requested: str | None = None) -> str:
+        """Conv operand precision of the attack engine: the request, else x6 (fp32-accurate bf16x6) for the
+        bmshj2018 / mbt2018 transforms and fp32 for cheng2020 (its k3 residual stacks have no x6 kernels)."""
+        if requested:
+            return requested
+        return "fp32" if self.model_kind == "cheng2020" else "x6"
+
     def kernels(self, precision: str = "fp32"):
         """Whole-model HIP executor (used by the attack engine).  precision 'bf16': bf16-operand g_a / g_s
         convs (bmshj2018 models; BASELINE config 5)."""

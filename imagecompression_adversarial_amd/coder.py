@@ -206,7 +206,9 @@ def config():
                    help="seeded CompressAI-init weights instead of the zoo download (offline)")
     p.add_argument("--batch", dest="batch", type=int, default=1,
                    help="attack this many same-size images per launch (per-image semantics preserved)")
-    p.add_argument("--precision", dest="precision", type=str, default="fp32", choices=("fp32", "bf16"),
-                   help="g_a/g_s conv operands: fp32 (exact, the reference dtype) or bf16 (MFMA bf16, fp32 "
-                        "accumulate; BASELINE config 5)")
+    p.add_argument("--precision", dest="precision", type=str, default=None, choices=("x6", "fp32", "bf16"),
+                   help="g_a/g_s conv operands: x6 (default for the bmshj2018 / mbt2018 models: fp32-accurate "
+                        "bf16x6 split-operand MFMA, error vs float64 no larger than the fp32-operand path's), fp32 "
+                        "(fp32-operand MFMA; the cheng2020 default) or bf16 (bf16 operands, fp32 accumulate; "
+                        "BASELINE config 5)")
     return p

@@ -470,7 +470,7 @@ def batch_attack(args):
     net = coder.load_model(args, training=False).to(args.device)
     for p in net.parameters():
         p.requires_grad_(False)
-    kern = net.kernels(getattr(args, "precision", "fp32"))
+    kern = net.kernels(net.attack_precision(getattr(args, "precision", None)))
     pre = args.method in ("resize", "bitdepth")
     bpp_ori_, bpp_, vi_, vi_pre_, n = 0.0, 0.0, 0.0, 0.0, 0
     for name, t, _, _ in _sources(args.source):
