@@ -383,7 +383,9 @@ def main():
     # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)
     traffic = None
     tfile = None
-    if args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "hyper":
+    if args.precision == "x6" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "hyper":
+        tfile = "pmc_traffic_x6.json"
+    elif args.precision == "fp32" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "hyper":
         tfile = "pmc_traffic.json"
     elif args.precision == "bf16" and (H, W, B) == (2048, 2048, 8):
         tfile = "pmc_traffic_c5.json"

@@ -426,12 +426,27 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       const unsigned vo_ld = valid ? vo : 0x0FFFFFF0u;  // past the descriptor's range: loads return 0
       float tw[8];   // x6: t of register quads g = 2k, 2k+1 (one k-step) before the split
       __builtin_amdgcn_sched_barrier(0);
+      // x6 (1 wave/SIMD): every (y, s) load of the tile in flight before the first use (left to itself the
+      // scheduler issued them two at a time, each pair behind an s_waitcnt vmcnt(0): 16 serialised HBM round
+      // trips per tile, ~35k cycles per conv_up class); the registers pass to t / 2x as the loads are consumed.
+      // The fp32 kernels run 2 waves/SIMD (the other wave covers the latency; the 128 registers would spill).
+      f32x4 yq[X6 ? IT : 1][4], sq[X6 ? IT : 1][4];
+      if constexpr (X6 != 0) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            yq[it][g] = IX.ld(vo_ld, so(it * 8 + 2 * g));
+            sq[it][g] = IS.ld(vo_ld, so(it * 8 + 2 * g));
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int it = 0; it < IT; ++it)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const unsigned ss = so(it * 8 + 2 * g);
-          const f32x4 yv = IX.ld(vo_ld, ss), sv = IS.ld(vo_ld, ss);
+          const f32x4 yv = X6 ? yq[X6 ? it : 0][g] : IX.ld(vo_ld, ss), sv = X6 ? sq[X6 ? it : 0][g] : IS.ld(vo_ld, ss);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float sg = sv[e], xs = yv[e] / sg;

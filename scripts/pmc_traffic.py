@@ -7,7 +7,7 @@ Our loads/stores are 16 B per lane (nChw4c float4), so both corrections apply as
 
 Kernels are identified by (name prefix, Grid_Size); the grids follow the launchers in ica_conv.hip.
     python scripts/pmc_traffic.py gpurun_out/pmc [B H W prec] > profiles/pmc_traffic.json
-(default: config 2 = 32 x 512x768 fp32; config 5 = 8 2048 2048 bf16).  Output {tag: bytes/launch}.
+(default: 32 x 512x768 fp32; config 2 x6 = 32 512 768 x6; config 5 = 8 2048 2048 bf16).  Output {tag: bytes/launch}.
 """
 import collections
 import csv
@@ -54,6 +54,33 @@ TAGS = {   # epilogue ids: 0 BIAS, 2 GDN, 3 IGDN, 4 GDN_BWD, 5 IGDN_BWD
     "g_a.6.dgrad": up(4, *h[4], N, 4), "g_a.4.dgrad": up(4, *h[3], N, 4), "g_a.2.dgrad": up(4, *h[2], N, 4),
     "g_a.0.dgrad": up3(*h[1]),
 }
+
+if PREC == "x6":   # ica_conv_x6.hip launchers (and the x6 Z-gather)
+    NS = "void (anonymous namespace)::"
+
+    def down_x6(epi, Hout, Wout, Cout, it):
+        return f"{NS}conv_down_x6_kernel<{it}, {epi}>", -(-Wout // 32) * -(-Hout // 8) * B * 256 * -(-Cout // (it * 32))
+
+    def rgb_x6(epi, Hout, Wout, Cout):
+        return f"{NS}conv_rgb_x6_kernel<4, {epi}>", -(-Wout // 32) * -(-Hout // 4) * B * 256 * -(-Cout // 128)
+
+    def up_x6(epi, Hin, Win, Cin, Cout):
+        cg = 128 if Cin <= 128 else 64
+        return f"{NS}conv_up_x6_kernel<4, {epi}, {cg}>", -(-Win // 16) * -(-Hin // 8) * B * 256 * -(-Cout // 128)
+
+    def up3_x6(Hin, Win):
+        return "void conv_up3_kernel<false, true>", -(-Win // 32) * -(-Hin // 5) * B * 256
+
+    TAGS = {
+        "g_a.0.fwd": rgb_x6(2, *h[1], N), "g_a.2.fwd": down_x6(2, *h[2], N, 4),
+        "g_a.4.fwd": down_x6(2, *h[3], N, 4), "g_a.6.fwd": down_x6(0, *h[4], M, 3),
+        "g_s.0.fwd": up_x6(3, *h[4], M, N), "g_s.2.fwd": up_x6(3, *h[3], N, N), "g_s.4.fwd": up_x6(3, *h[2], N, N),
+        "g_s.6.fwd": up3_x6(*h[1]),
+        "g_s.6.dgrad": rgb_x6(5, *h[1], N), "g_s.4.dgrad": down_x6(5, *h[2], N, 4),
+        "g_s.2.dgrad": down_x6(5, *h[3], N, 4), "g_s.0.dgrad": down_x6(0, *h[4], M, 3),
+        "g_a.6.dgrad": up_x6(4, *h[4], M, N), "g_a.4.dgrad": up_x6(4, *h[3], N, N), "g_a.2.dgrad": up_x6(4, *h[2], N, N),
+        "g_a.0.dgrad": up3_x6(*h[1]),
+    }
 
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/p*/*_counter_collection.csv"):
