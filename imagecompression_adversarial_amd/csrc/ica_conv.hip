@@ -22,6 +22,25 @@
 //               wave runs two class tiles paired 9+4 / 6+6 for balance.
 #include "ica_conv_epi.h"
 
+#ifdef ICA_BF_TRACE
+// phase timestamps (s_memtime cycles) per (block, wave): experiment builds only (scripts/exp/bf_trace.py)
+__device__ unsigned long long ica_bf_trace[32768 * 4 * 8];
+#define BFT(k)                                                                                                 \
+  do {                                                                                                         \
+    if ((threadIdx.x & 63) == 0) {                                                                             \
+      const unsigned b_ = blockIdx.x + gridDim.x * blockIdx.y;                                                 \
+      if (b_ < 32768) ica_bf_trace[((size_t)b_ * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_readcyclecounter(); \
+    }                                                                                                          \
+  } while (0)
+extern "C" int ica_bf_trace_read(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ica_bf_trace), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define BFT(k) \
+  do {         \
+  } while (0)
+#endif
+
 // bf16 weight-fragment load of tile it at step g
 #define ICA_WLOAD_BF(w, it, g) ((w)[(it) * 64])
 
@@ -104,6 +123,7 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
   for (int t = 0; t < PT; ++t)
 #pragma unroll
     for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
+  BFT(0);
 
   // one 4-channel group of the conv input at (iy, ix), with the fill-mode view applied
   auto ldc4 = [&](int c4, int iy, int ix) -> f32x4 {
@@ -356,6 +376,7 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
     if (g < total) step(fr[0], fr[3], g);
     if (g + 1 < total) step(fr[1], fr[0], g + 1);
     if (g + 2 < total) step(fr[2], fr[1], g + 2);
+    BFT(2);
   } else if constexpr (CC == 4) {
     // fp32 RGB input, packed K (pack_conv_kernel, CC = 4): k-step m = 2g + s2 of step g takes the (tap,
     // channel) pair f = 2m + h from lane half h, f running over tap*Cin + channel.  With Cin = 3 that is
@@ -435,6 +456,7 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
     const int oy = oy0 + oyl[t], ox = ox0 + oxl[t];
     conv_epilogue<IT, EPI, FX, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
   }
+  BFT(3);
 }
 
 // --------------------------------------------------------------------------
@@ -588,10 +610,13 @@ ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], 
 
 template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF>
 ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a0, int b0, int jt, int cb,
-                           int nch) {
+                           int nch, int tk) {
   f32x16 acc[up_pt<BF>()][IT];
   conv_up_acc<KS, PY, PX, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc);
+  BFT(tk);
   conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb);
+  BFT(tk + 1);
+  (void)tk;
 }
 
 // fp32 forward epilogues (stores only): both classes' main loops first, then both epilogues.  The first class's
@@ -614,9 +639,9 @@ ICA_DEV void conv_up_pair(const ConvParams& p, const f32x4* patch, int n, int a0
     conv_up_store<PY0, PX0, IT, EPI, FX, BF>(p, acc0, n, a0, b0, jt, cb);
     conv_up_store<PY1, PX1, IT, EPI, FX, BF>(p, acc1, n, a0, b0, jt, cb);
   } else {
-    conv_up_class<KS, PY0, PX0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, PY0, PX0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
-    conv_up_class<KS, PY1, PX1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+    conv_up_class<KS, PY1, PX1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch, 4);
   }
 }
 
@@ -638,6 +663,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   // The patch fill: batches of UP_FB entries per thread whose loads are all issued before their LDS writes
   // (buffer loads with 32-bit offsets into this image; padding pixels read past the descriptor and get
   // zeros), so the fill costs one memory latency per batch instead of one per entry.
+  BFT(0);
   const unsigned xplane = (unsigned)p.Hin * p.Win;
   const unsigned qbytes = BF ? 8u : 16u;
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(
@@ -668,6 +694,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
     }
   }
   __syncthreads();
+  BFT(1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int jt = wave & 1, nch = p.Cin / 16;
   // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
