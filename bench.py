@@ -142,6 +142,9 @@ def _tag_prec(kern):
     return out
 
 
+_PREC_NAME = {0: "fp32", 1: "bf16", 2: "x6"}
+
+
 def _peak(prec):
     return {1: BF16_MFMA_PEAK_TFLOPS, 2: X6_PEAK_TFLOPS}.get(prec, FP32_MFMA_PEAK_TFLOPS)
 
@@ -195,8 +198,9 @@ def bench_finetune(args):
     lmbda = LAMBS[metric][q - 1]
     tr = RDTrainer(net, metric, lmbda)
     group = dist.group.WORLD if dist else None
+    fprec = net.attack_precision(args.precision)
     fargs = SimpleNamespace(steps=inner, epsilon=16.0, noise=1e-4, lr_attack=0.01, att_metric="L2", clamp=True,
-                            round_adv=False)
+                            round_adv=False, precision=fprec)
     gen = torch.Generator(device=dev).manual_seed(rank)
     xs = [torch.rand((B, 3, H, W), generator=gen, device=dev) for _ in range(args.warmup + args.steps)]
     for i in range(args.warmup):
@@ -206,6 +210,7 @@ def bench_finetune(args):
         dist.barrier()
     K.EVENT_HOOK = {}
     K.FLOPS_HOOK = {}
+    K.PREC_HOOK = {}
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         adv_step(net, tr, opt, aux, xs[i], fargs, group, world)
@@ -229,8 +234,10 @@ def bench_finetune(args):
         if tag is None:
             return None
         ach = tot_fl[tag] / (tot_ms[tag] * 1e-3) / 1e12
-        return {"bound": "mfma", "kernel": tag, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+        pk = _peak(K.PREC_HOOK.get(tag, 0))   # the operands that tag's launches ran on
+        return {"bound": "mfma", "kernel": tag, "achieved": round(ach, 2), "peak": pk,
+                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": None, "operands": _PREC_NAME[
+                    K.PREC_HOOK.get(tag, 0)],
                 "launch_ms": round(tot_ms[tag] / len(hook[tag]), 4),
                 "flops_per_launch": tot_fl[tag] / len(hook[tag])}
     ms_outer = el / args.steps * 1e3
@@ -241,7 +248,9 @@ def bench_finetune(args):
                       "second over whole outer steps (inner attack + RD train step + grad all-reduce + Adam)",
             "value": round(value, 3), "unit": "attack-step·images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_outer, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
+            "vs_baseline": None,
+            "dtype": ("f32 (inner attack: fp32-accurate x6 operands on the large layers, fp32 MFMA on the small-grid "
+                      "ones; train step fp32 MFMA)" if fprec == "x6" else "f32"),
             "data": "synthetic (torch.rand 256x256 crops, seeded CompressAI-init weights)",
             "config": {"workload": f"train.py --adv -m hyper -q {q} -metric {metric} -steps {inner} -lamb {lmbda}, "
                                    f"{B} images/GPU of {W}x{H}, one outer step per timed step",
@@ -347,6 +356,7 @@ def main():
     if dist:
         dist.barrier()
     K.EVENT_HOOK = {}
+    K.PREC_HOOK = {}
     K.FLOPS_HOOK = {}
     exp0 = loop.expensive_image_steps()
     torch.cuda.synchronize()
@@ -377,7 +387,7 @@ def main():
     dom_ms = per_tag[dom] if dom else 0.0
     dom_flops = tot_fl[dom] / len(hook[dom]) if dom else 0.0
     achieved = tot_fl[dom] / (tot_ms[dom] * 1e-3) / 1e12 if dom else 0.0
-    tag_prec = _tag_prec(kern) if model == "hyper" else {}
+    tag_prec = (dict(K.PREC_HOOK) or _tag_prec(kern)) if model == "hyper" else {}
     peak = _peak(tag_prec.get(dom, 0))
     # HBM bytes per launch of the dominant kernel from the committed PMC passes of the same shapes
     # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)

@@ -20,6 +20,8 @@
 //               parity classes (9/6/6/4 taps).  Block = 8x32 output pixels
 //               (4x16 per class); the whole-Cin input patch lives in LDS; each
 //               wave runs two class tiles paired 9+4 / 6+6 for balance.
+#include <type_traits>
+
 #include "ica_conv_epi.h"
 
 #ifdef ICA_BF_TRACE
@@ -96,6 +98,10 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
   // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
   __shared__ f32x4 patch[NE * PLANE];
+  // bf16 16-channel-chunk layers: the epilogue parameters in LDS (epi_params_to_lds), copied before the first
+  // chunk fill, whose barriers publish them
+  constexpr bool LG = BF && CC == 16 && FX == 0;
+  __shared__ f32x4 lpar[LG ? epi_lds_entries<IT, EPI>() : 1];
 
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
   int bid, cb;
@@ -109,6 +115,7 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
   const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
   const int Cin4 = (p.Cin + 3) >> 2;
   const int nch = (Cin4 * 4 + CC - 1) / CC;
+  if constexpr (LG) epi_params_to_lds<IT, EPI>(p, lpar, cb * IT * 32);
   // pixel tile t of this wave: block pixels (wave*PT + t)*32 + j
   int oyl[PT], oxl[PT];
 #pragma unroll
@@ -454,9 +461,132 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = oy0 + oyl[t], ox = ox0 + oxl[t];
-    conv_epilogue<IT, EPI, FX, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+    conv_epilogue<IT, EPI, FX, BF, 0, LG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lpar);
   }
   BFT(3);
+}
+
+// --------------------------------------------------------------------------
+// Small-grid fp32 conv_down (16-channel chunks, plain view): the 4 waves of a block share ONE 32-pixel output
+// tile (4 x 8) and split its taps (wave w: taps [w KK / 4, (w + 1) KK / 4)); the four partial accumulators are
+// summed through LDS in wave order (deterministic) and wave 0 runs the epilogue.  4x the blocks of
+// conv_down_kernel and a quarter of its serial MFMA chain per wave, for the layers whose plain grid leaves most
+// CUs idle (the fine-tune's 256x256 crops: 16x16 .. 64x64 outputs, 32-256 blocks), where the plain kernel runs at
+// the latency of one wave's K chain.  Weights: the conv_down pack ([cb][chunk][tap][it][lane][8]).
+// --------------------------------------------------------------------------
+constexpr int DS_TW = 8, DS_TH = 4;
+template <int KS, int S, int IT, int EPI, int FX>
+__global__ __launch_bounds__(256, 2) void conv_down_split_kernel(ConvParams p) {
+  constexpr int PR = S * (DS_TH - 1) + KS, PC = S * (DS_TW - 1) + KS, PLANE = PR * PC, PAD = KS / 2;
+  constexpr int KK = KS * KS, NQ = 4, KH = 8, WSTEP = IT * 64 * KH;
+  constexpr int NF = (NQ * PLANE + 255) / 256;
+  __shared__ f32x4 patch[NQ * PLANE];
+  __shared__ f32x4 red[3 * IT * 4 * 64];   // partial accumulators of waves 1..3: [wave-1][it][quad][lane]
+  const int tiles_x = (p.Wout + DS_TW - 1) / DS_TW, tiles_y = (p.Hout + DS_TH - 1) / DS_TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5,
+            j = lane & 31;
+  const int oy0 = ty * DS_TH, ox0 = tx * DS_TW;
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int Cin4 = (p.Cin + 3) >> 2, nch = (Cin4 * 4 + 15) / 16;
+  const int oyl = j / DS_TW, oxl = j % DS_TW;
+  const int lbase = S * oyl * PC + S * oxl;
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  // chunk fill: every entry of this thread loaded before the barrier that ends the previous chunk's reads
+  auto fill = [&](int ch) {
+    u32x4_t v[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+      const int iy = iy0 + pr, ix = ix0 + pc, c4 = ch * NQ + q;
+      const bool ok = e < NQ * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e < NQ * PLANE) patch[e] = __builtin_bit_cast(f32x4, v[i]);
+    }
+    __syncthreads();
+  };
+  f32x16 acc[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+  const int t0 = wave * KK / 4, t1 = (wave + 1) * KK / 4, nt = t1 - t0;
+  const float* wptr = p.wp + (size_t)cb * nch * KK * WSTEP + (size_t)lane * KH;
+  // step u of this wave = (chunk u / nt, tap t0 + u % nt); weights one step ahead (ping-pong)
+  auto goff = [&](int u) -> size_t {
+    const int ch = u / nt, t = t0 + (u - ch * nt);
+    return ((size_t)ch * KK + t) * WSTEP;
+  };
+  const int total = nch * nt;
+  auto step = [&](float (&cur)[IT][KH], float (&nxt)[IT][KH], int u) {
+    const int ch = u / nt, tap = t0 + (u - ch * nt);
+    load_frag<IT, KH>(nxt, wptr + goff(min(u + 1, total - 1)));
+    const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+    const int lo = lbase + ky * PC + kx;
+    const f32x4 v0 = patch[(2 * h) * PLANE + lo], v1 = patch[(2 * h + 1) * PLANE + lo];
+    const float b[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+    for (int s2 = 0; s2 < KH; ++s2)
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[it] = mfma32(cur[it][s2], b[s2], acc[it]);
+  };
+  float fa[IT][KH], fb[IT][KH];
+  load_frag<IT, KH>(fa, wptr + goff(0));
+  // every wave joins every chunk's fill (the barriers); a chunk is nt steps of this wave
+  int u = 0;
+#pragma unroll 1
+  for (int ch = 0; ch < nch; ++ch) {
+    fill(ch);
+    const int ue = u + nt;
+#pragma unroll 1
+    for (; u + 1 < ue; u += 2) {
+      step(fa, fb, u);
+      step(fb, fa, u + 1);
+    }
+    if (u < ue) {   // odd step count: swap the roles by copying the prefetched set (once per chunk)
+      step(fa, fb, u);
+      ++u;
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int k = 0; k < KH; ++k) fa[it][k] = fb[it][k];
+    }
+  }
+  // fixed-order reduction: waves 1..3 park their partial sums, wave 0 adds them in wave order
+  if (wave > 0) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        red[(((wave - 1) * IT + it) * 4 + g) * 64 + lane] =
+            f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]};
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 r = red[((w * IT + it) * 4 + g) * 64 + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
+      }
+  const int oy = oy0 + oyl, ox = ox0 + oxl;
+  conv_epilogue<IT, EPI, FX, false>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
 // --------------------------------------------------------------------------
@@ -475,15 +605,20 @@ constexpr int up_th() { return 4 * up_pt<BF>(); }
 template <bool BF>
 constexpr int up_plane() { return (up_th<BF>() + 2) * UP_PC; }
 
+// bf16: the epilogue parameters (epi_params_to_lds) sit in LDS right after the whole-Cin patch
+template <bool BF>
+ICA_DEV const f32x4* up_lpar(const f32x4* patch, int nch) { return BF ? patch + 2 * nch * up_plane<BF>() : nullptr; }
+
 // Generalised over the kernel size: ConvTranspose2d kKS s2 p(KS/2) op1, i.e. the input-gradient
 // of a stride-2 KSxKS conv with pad KS/2 (KS = 5: g_s deconvs / g_a dgrad; KS = 3, 1: the dgrad of
 // cheng2020's conv3x3 s2 and conv1x1 s2 skips).  Output y = 2a + PY uses taps
 // ky = ky0 + 2i, ky0 = (PY + PAD) & 1, at input row iy = a + (PY + PAD - ky) / 2 in [a-1, a+1].
-template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF>
+// TH: input rows of the block tile (the patch holds TH + 2 rows)
+template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF, int TH = up_th<BF>()>
 ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch,
                          f32x16 (&acc)[up_pt<BF>()][IT]) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-  constexpr int PT = up_pt<BF>(), UP_PLANE = up_plane<BF>();
+  constexpr int PT = up_pt<BF>(), UP_PLANE = (TH + 2) * UP_PC;
   // pixel tile t of this wave: input rows (jt*PT + t)*2 + (j>>4) of the block tile, columns j&15
   const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
   constexpr int WSTEP = IT * 64 * 8;
@@ -597,14 +732,14 @@ ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb
 // the epilogue of class (PY, PX) for the pixel tiles of row group jt
 template <int PY, int PX, int IT, int EPI, int FX, bool BF>
 ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], int n, int a0, int b0, int jt,
-                           int cb) {
+                           int cb, const f32x4* lp) {
   constexpr int PT = up_pt<BF>();
   const int j = threadIdx.x & 31;
   const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-    conv_epilogue<IT, EPI, FX, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+    conv_epilogue<IT, EPI, FX, BF, 0, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lp);
   }
 }
 
@@ -614,7 +749,7 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
   f32x16 acc[up_pt<BF>()][IT];
   conv_up_acc<KS, PY, PX, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc);
   BFT(tk);
-  conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb);
+  conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
   BFT(tk + 1);
   (void)tk;
 }
@@ -636,8 +771,8 @@ ICA_DEV void conv_up_pair(const ConvParams& p, const f32x4* patch, int n, int a0
     __builtin_amdgcn_sched_barrier(0);
     conv_up_acc<KS, PY1, PX1, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc1);
     __builtin_amdgcn_sched_barrier(0);
-    conv_up_store<PY0, PX0, IT, EPI, FX, BF>(p, acc0, n, a0, b0, jt, cb);
-    conv_up_store<PY1, PX1, IT, EPI, FX, BF>(p, acc1, n, a0, b0, jt, cb);
+    conv_up_store<PY0, PX0, IT, EPI, FX, BF>(p, acc0, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
+    conv_up_store<PY1, PX1, IT, EPI, FX, BF>(p, acc1, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
   } else {
     conv_up_class<KS, PY0, PX0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
@@ -669,6 +804,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(
       reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * qbytes, Cin4 * xplane * qbytes);
   constexpr int UP_FB = 8;
+  if constexpr (BF) epi_params_to_lds<IT, EPI>(p, patch + total, cb * IT * 32);   // published by the fill's barrier
   for (int e0 = threadIdx.x; e0 < total; e0 += 256 * UP_FB) {
     u32x4_t v[UP_FB];
 #pragma unroll
@@ -702,6 +838,69 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
     conv_up_pair<KS, 0, 0, 1, 1, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   } else {
     conv_up_pair<KS, 0, 1, 1, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
+  }
+}
+
+// --------------------------------------------------------------------------
+// Small-grid fp32 conv_up: the block owns ONE 32-pixel input tile (2 x 16) and wave w computes output-parity
+// class (w >> 1, w & 1) of it (9 / 6 / 6 / 4 taps).  Twice the blocks of conv_up_kernel (64-pixel tiles, two
+// classes per wave) and at most 9 instead of 13 taps of serial MFMA chain per wave: for the layers whose plain
+// grid leaves most CUs idle (the fine-tune's 256x256 crops: 16x16 .. 64x64 inputs, 32-512 blocks), which run at
+// the latency of one wave's K chain.  Same accumulation order per output element as conv_up_kernel.
+// --------------------------------------------------------------------------
+constexpr int UPS_TH = 2, UPS_PLANE = (UPS_TH + 2) * UP_PC;
+template <int KS, int IT, int EPI, int FX>
+__global__ __launch_bounds__(256, 2) void conv_up_small_kernel(ConvParams p) {
+  extern __shared__ f32x4 patch[];  // [Cin/4][UPS_TH + 2][UP_PC]
+  const int Hh = p.Hin, Wh = p.Win;
+  const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UPS_TH - 1) / UPS_TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int a0 = ty * UPS_TH, b0 = tx * UP_TW;
+  const int Cin4 = p.Cin >> 2;  // Cin % 16 == 0 enforced by host
+  const int total = Cin4 * UPS_PLANE;
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  constexpr int FB = 8;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * FB) {
+    u32x4_t v[FB];
+#pragma unroll
+    for (int i = 0; i < FB; ++i) {
+      const int e = e0 + 256 * i;
+      const int q = e / UPS_PLANE, rem = e - q * UPS_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
+      const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+      const bool ok = e < total && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)q * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < FB; ++i) {
+      const int e = e0 + 256 * i;
+      if (e < total) patch[e] = __builtin_bit_cast(f32x4, v[i]);
+    }
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nch = p.Cin / 16;
+  auto run = [&](auto py_c, auto px_c) __attribute__((always_inline)) {
+    constexpr int PY = decltype(py_c)::value, PX = decltype(px_c)::value;
+    f32x16 acc[1][IT];
+    conv_up_acc<KS, PY, PX, IT, EPI, FX, false, UPS_TH>(p, patch, 0, cb, nch, acc);
+    const int j = threadIdx.x & 31;
+    const int oy = 2 * (a0 + (j >> 4)) + PY, ox = 2 * (b0 + (j & 15)) + PX;
+    conv_epilogue<IT, EPI, FX, false>(p, acc[0], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  switch (wave) {
+    case 0: run(I0{}, I0{}); break;
+    case 1: run(I0{}, I1{}); break;
+    case 2: run(I1{}, I0{}); break;
+    default: run(I1{}, I1{}); break;
   }
 }
 
@@ -1126,8 +1325,23 @@ static int launch_down(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
+// small-grid variant (conv_down_split_kernel): outputs of at most 64 x 64 pixels per image.  A per-image
+// criterion, so image b of a batch runs the same kernel (and rounds identically) at any batch size.
+constexpr int DOWN_SMALL_PX = 64 * 64, UP_SMALL_PX = 64 * 64;
+template <int KS, int S, int IT, int EPI, int FX>
+static int launch_down_split(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Wout + DS_TW - 1) / DS_TW) * ((p.Hout + DS_TH - 1) / DS_TH) * p.N;
+  dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
+  hipLaunchKernelGGL((conv_down_split_kernel<KS, S, IT, EPI, FX>), grid, dim3(256), 0, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int KS, int S, int IT, int CC, int EPI, int FX, bool BF = false>
 static int pick_tw_down(const ConvParams& p, hipStream_t st) {
+  if constexpr (!BF && CC == 16 && KS == 5 && S == 2 && (FX == 0 || FX == FX_T) && (IT == 3 || IT == 4 || IT == 6)) {
+    if (p.Hout * p.Wout <= DOWN_SMALL_PX) return launch_down_split<KS, S, IT, EPI, FX>(p, st);
+  }
   if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<KS, S, IT, CC, 32, EPI, FX, BF>(p, st);
   return launch_down<KS, S, IT, CC, 16, EPI, FX, BF>(p, st);
 }
@@ -1218,13 +1432,35 @@ static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, int fx
   return -6;
 }
 
+template <int KS, int IT, int EPI, int FX>
+static int launch_up_small(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UPS_TH - 1) / UPS_TH) * p.N;
+  dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
+  const size_t lds = (size_t)(p.Cin / 4) * UPS_PLANE * sizeof(f32x4);
+  if (lds > 160 * 1024) return -2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_small_kernel<KS, IT, EPI, FX>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_up_small_kernel<KS, IT, EPI, FX>), grid, dim3(256), lds, st, p);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int KS, int IT, int EPI, int FX, bool BF = false>
 static int launch_up(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
+  // small grids (inputs of at most 64 x 64 pixels per image): one class per wave over 32-pixel tiles
+  if constexpr (!BF && KS == 5 && (FX == 0 || FX == FX_T) && (IT == 4 || IT == 6)) {
+    if (p.Hin * p.Win <= UP_SMALL_PX) return launch_up_small<KS, IT, EPI, FX>(p, st);
+  }
   constexpr int UP_TH = up_th<BF>();
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  const size_t lds = (size_t)(p.Cin / (BF ? 8 : 4)) * up_plane<BF>() * sizeof(f32x4);
+  const size_t lds = ((size_t)(p.Cin / (BF ? 8 : 4)) * up_plane<BF>() + (BF ? epi_lds_entries<IT, EPI>() : 0)) *
+                     sizeof(f32x4);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {

@@ -100,6 +100,48 @@ ICA_DEV void split3x8(const float (&v)[8], bf16x8 (&o)[3]) {
 }
 
 // --------------------------------------------------------------------------
+// Epilogue parameters in LDS (bf16 kernels).  vmcnt counts loads and stores together in issue order, so every
+// bias / beta' / gamma' load an epilogue issues after one of its own stores waits for that store to complete:
+// the bf16 conv_up epilogues (one parameter load per channel quad or normaliser tile between stores) ran as a
+// chain of store round trips, ~20-40k cycles per class (phase stamps, scripts/exp/bf_trace.py).  The block copies
+// the parameters into LDS once, next to its patch fill; the epilogue then reads them with ds_read (lgkmcnt), which
+// never waits on a store.  Layout in 16-B entries: [0, 8 IT) bias quads of channels co_base.., [8 IT, 16 IT)
+// beta' quads (GDN / IGDN forward), then the bf16 gamma' (forward) / gamma'^T (backward) hi fragments,
+// entry k * 64 + lane for k = (a * IT + b) * 2 + s (the global pack's 1-KB piece at byte k * 2048).
+// --------------------------------------------------------------------------
+template <int EPI>
+constexpr bool epi_gdn() { return EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD; }
+template <int IT, int EPI>
+constexpr int epi_lds_entries() { return 16 * IT + (epi_gdn<EPI>() ? IT * IT * 128 : 0); }
+
+template <int IT, int EPI>
+ICA_DEV void epi_params_to_lds(const ConvParams& p, f32x4* lp, int co_base) {
+  constexpr int NG = epi_gdn<EPI>() ? IT * IT * 128 : 0, NP = 16 * IT;
+  constexpr int NI = (NP + NG + 255) / 256;
+  const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout);
+  const __amdgpu_buffer_rsrc_t ers = chan_rsrc((EPI == EPI_GDN || EPI == EPI_IGDN) ? p.beta : nullptr, p.Cout);
+  const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(epi_gdn<EPI>() ? p.gp : nullptr, epi_gdn<EPI>() ? IT * IT * 4096 : 0);
+  f32x4 v[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (e < 8 * IT) v[i] = ld_chan4(brs, co_base + 4 * e);
+    else if (e < NP) v[i] = ld_chan4(ers, 4 * (e - 8 * IT));
+    else if (e < NP + NG) {   // gamma' pieces: byte (k * 2048 + l * 16) < IT * IT * 4096
+      const int k = (e - NP) >> 6, l = (e - NP) & 63;
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(grs, k * 2048 + l * 16, 0, 0));
+    } else {
+      v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (e < NP + NG) lp[e] = v[i];
+  }
+}
+
+// --------------------------------------------------------------------------
 // Epilogue: acc[it] holds channels co_base + it*32 + acc_row(r,h) of pixel
 // (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
 // float4 of channel group c4 = co_base/4 + it*8 + 2g + h.
@@ -109,9 +151,11 @@ ICA_DEV void split3x8(const float (&v)[8], bf16x8 (&o)[3]) {
 // register file): all IT output tiles at once, gamma' fragments one round ahead; X6 = 2 ("narrow", for kernels
 // at 2 waves/SIMD, 256 registers): one output tile at a time, the other wave hides the fragment latency.
 // the three-plane gamma' pack of ica_pack_gdn_x6 (p.gp), fp32-accurate like the main loop of the x6 kernels.
-template <int IT, int EPI, int FX, bool BF = false, int X6 = 0>
+// LG: the epilogue parameters come from the block's epi_params_to_lds copy at lp (bf16 kernels); otherwise from
+// global memory
+template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
-                           bool valid, int co_base) {
+                           bool valid, int co_base, const f32x4* lp = nullptr) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int C4o = (p.Cout + 3) >> 2;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
@@ -138,12 +182,23 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     const Img SX((FX & FX_RES) ? p.save_x : nullptr, img, n);
     const Img RS((FX & FX_RES) ? p.res : nullptr, img, n);
     const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout);
+    // x6 kernels (1 wave/SIMD, registers to spare): every bias quad loaded before the first store (a load issued
+    // after a store waits for it: vmcnt is in order)
+    constexpr bool PRE = X6 != 0 && !LG;
+    f32x4 bvs[PRE ? IT : 1][4];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bvs[it][g] = ld_chan4(brs, co_base + it * 32 + 8 * g + 4 * h);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c0 = co_base + it * 32 + 8 * g + 4 * h;
-        const f32x4 bv = ld_chan4(brs, c0);
+        const f32x4 bv = LG ? lp[it * 8 + 2 * g + h] : PRE ? bvs[PRE ? it : 0][g] : ld_chan4(brs, c0);
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -203,7 +258,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 bv = ld_chan4(brs, it * 32 + 8 * g + 4 * h);   // channels acc_row(4g + e, h)
+        const f32x4 bv = LG ? lp[it * 8 + 2 * g + h] : ld_chan4(brs, it * 32 + 8 * g + 4 * h);   // channels acc_row(4g + e, h)
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += bv[e];
       }
@@ -263,13 +318,15 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     }
 #pragma unroll
     for (int ct = 0; ct < IT; ++ct) {
+      // LDS parameters: one normaliser tile per scheduling region (hoisting every tile's gamma' reads spilled)
+      if constexpr (LG) __builtin_amdgcn_sched_barrier(0);
       f32x16 nacc;
       if constexpr (X6 == 1) {
         nacc = nx[ct];
       } else {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
+          const f32x4 ev = LG ? lp[8 * IT + ct * 8 + 2 * g + h] : ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) nacc[4 * g + e] = ev[e];
         }
@@ -307,9 +364,11 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
       for (int it = 0; it < (X6 ? 0 : IT); ++it) {
         if constexpr (BF) {
-          const int o = (ct * IT + it) * 4096;
+          const int o = (ct * IT + it) * 4096, k0 = (ct * IT + it) * 2;
 #pragma unroll
-          for (int s = 0; s < 2; ++s) nacc = mfma32bf(ld_bf8(grs, lane * 16, o + s * 2048), xh[it][s], nacc);
+          for (int s = 0; s < 2; ++s)
+            nacc = mfma32bf(LG ? f4_as_bf8(lp[16 * IT + (k0 + s) * 64 + lane]) : ld_bf8(grs, lane * 16, o + s * 2048),
+                            xh[it][s], nacc);
         } else {
           const float* gq = p.gp + ((size_t)(ct * IT + it) * 64 + lane) * 16;
           const f32x4 g0 = ld4(gq), g1 = ld4(gq + 4), g2 = ld4(gq + 8), g3 = ld4(gq + 12);
@@ -403,9 +462,11 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         f32x16 uacc = f32x16{0};
 #pragma unroll
         for (int ct = 0; ct < IT; ++ct) {
-          const int o = (jt * IT + ct) * 4096;
+          const int o = (jt * IT + ct) * 4096, k0 = (jt * IT + ct) * 2;
 #pragma unroll
-          for (int s = 0; s < 2; ++s) uacc = mfma32bf(ld_bf8(grs, lane * 16, o + s * 2048), th[ct][s], uacc);
+          for (int s = 0; s < 2; ++s)
+            uacc = mfma32bf(LG ? f4_as_bf8(lp[16 * IT + (k0 + s) * 64 + lane]) : ld_bf8(grs, lane * 16, o + s * 2048),
+                            th[ct][s], uacc);
         }
         if (valid) {
 #pragma unroll

@@ -42,6 +42,16 @@ def _ev_end(h, flops=None):
             FLOPS_HOOK[h[0]] = flops / max(h[2], 1)
 
 
+# operand precision of each tagged conv launch (filled while EVENT_HOOK is set): what actually ran, small-grid
+# fp32 fallbacks of x6 layers included
+PREC_HOOK = {}
+
+
+def _prec_note(tag, prec):
+    if EVENT_HOOK is not None and tag is not None:
+        PREC_HOOK[tag] = prec
+
+
 # algorithmic FLOPs PER IMAGE of each tagged ica_conv_ex launch (filled while EVENT_HOOK is set): 2*MAC of the
 # conv (a transposed conv counts the MACs of the conv it differentiates) + the GDN channel GEMM if fused
 FLOPS_HOOK = {}
@@ -258,6 +268,8 @@ class PackedConv:
         keep the fp32 packs."""
         fp = PackedConv(weight, bias, kind, stride, PREC_FP32, self.it_fwd, self.it_bwd)
         self.__dict__.update(fp.__dict__)
+        # the fp32 packs stay: small grids (sel_fwd / sel_bwd) run the fp32 small-grid kernels
+        self.fwd32, self.bwd32 = fp.fwd, fp.bwd
         if self.KS != 5 or stride != 2:
             return
         KK = 25
@@ -288,6 +300,25 @@ class PackedConv:
             elif x6_ok(self.Cin, self.Cout, self.it_bwd):       # dgrad conv_down: o = ci, c = co
                 self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, x6_it(self.Cin))
                 self.bwd_prec = PREC_X6
+
+
+    # x6 launches whose low-resolution side (conv_down output / conv_up input) has at most X6_SMALL_PX pixels per
+    # image run the fp32 small-grid kernels instead (conv_down_split_kernel / conv_up_small_kernel, fp32 MFMA): an
+    # x6 block covers 256 pixels at one block per CU, so such layers (the fine-tune's 256x256 crops below 64x64)
+    # would leave most CUs idle.  A per-image rule: image b of a batch runs the same kernels at any batch size.
+    X6_SMALL_PX = 32 * 32
+
+    def sel_fwd(self, lowres_px: int):
+        """(pack, prec) of the forward launch for a layer whose low-resolution side has lowres_px pixels."""
+        if self.fwd_prec == PREC_X6 and lowres_px <= self.X6_SMALL_PX and getattr(self, "fwd32", None) is not None:
+            return self.fwd32, PREC_FP32
+        return self.fwd, self.fwd_prec
+
+    def sel_bwd(self, lowres_px: int):
+        """(pack, prec) of the input-gradient launch (see sel_fwd)."""
+        if self.bwd_prec == PREC_X6 and lowres_px <= self.X6_SMALL_PX and getattr(self, "bwd32", None) is not None:
+            return self.bwd32, PREC_FP32
+        return self.bwd, self.bwd_prec
 
 
 class PackedGDN:
@@ -341,6 +372,7 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex).
     it: the row-tile count wp was packed with (0 = library default; explicit values go through ica_conv_ex)."""
     N, _, H, W, _ = x4.shape
+    _prec_note(tag, prec)
     if prec in (PREC_BF16, PREC_X6) or it:
         return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
@@ -366,6 +398,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
             out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
+    _prec_note(tag, prec)
     if (prec in (PREC_BF16, PREC_X6) or it) and Cout != 3:
         return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho, Wo = 2 * H, 2 * W

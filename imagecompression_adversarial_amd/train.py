@@ -87,7 +87,9 @@ def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, g
     B_global = D.global_count(B_local, batch_x.device, group)
     for p in net.parameters():
         p.requires_grad_(False)
-    res = attack_batch(net.kernels(), batch_x, steps=args.steps, epsilon=args.epsilon, noise_thr=args.noise,
+    # the inner attack runs on the attack engine's precision (x6 by default for bmshj2018: fp32-accurate)
+    kern = net.kernels(net.attack_precision(getattr(args, "precision", None)))
+    res = attack_batch(kern, batch_x, steps=args.steps, epsilon=args.epsilon, noise_thr=args.noise,
                        lr=args.lr_attack, att_metric=args.att_metric, clamp=args.clamp, eval_msssim=False,
                        coupled=True, group=group)
     for p in net.parameters():
