@@ -20,6 +20,7 @@
 //               parity classes (9/6/6/4 taps).  Block = 8x32 output pixels
 //               (4x16 per class); the whole-Cin input patch lives in LDS; each
 //               wave runs two class tiles paired 9+4 / 6+6 for balance.
+#include <algorithm>
 #include <type_traits>
 
 #include "ica_conv_epi.h"
@@ -575,8 +576,8 @@ __global__ __launch_bounds__(256, 2) void conv_down_split_kernel(ConvParams p) {
   }
   __syncthreads();
   if (wave != 0) return;
-#pragma unroll
-  for (int w = 0; w < 3; ++w)
+#pragma unroll 1
+  for (int w = 0; w < 3; ++w) {   // one partial at a time (all LDS reads hoisted spilled)
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -585,6 +586,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_split_kernel(ConvParams p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
       }
+  }
   const int oy = oy0 + oyl, ox = ox0 + oxl;
   conv_epilogue<IT, EPI, FX, false>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
@@ -615,8 +617,9 @@ ICA_DEV const f32x4* up_lpar(const f32x4* patch, int nch) { return BF ? patch + 
 // ky = ky0 + 2i, ky0 = (PY + PAD) & 1, at input row iy = a + (PY + PAD - ky) / 2 in [a-1, a+1].
 // TH: input rows of the block tile (the patch holds TH + 2 rows)
 template <int KS, int PY, int PX, int IT, int EPI, int FX, bool BF, int TH = up_th<BF>()>
+// c0, cn (fp32 only): accumulate input-channel chunks [c0, c0 + cn) of the nch (cn = 0: all of them)
 ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch,
-                         f32x16 (&acc)[up_pt<BF>()][IT]) {
+                         f32x16 (&acc)[up_pt<BF>()][IT], int c0 = 0, int cn = 0) {
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   constexpr int PT = up_pt<BF>(), UP_PLANE = (TH + 2) * UP_PC;
   // pixel tile t of this wave: input rows (jt*PT + t)*2 + (j>>4) of the block tile, columns j&15
@@ -630,15 +633,16 @@ ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb
 #pragma unroll
     for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
   // (tap, chunk) sequence flattened
-  const int total = NY * NX * nch;
+  const int ncw = cn > 0 ? cn : nch;
+  const int total = NY * NX * ncw;
   auto woff = [&](int u) -> size_t {
-    const int ti = u / nch, ch = u - ti * nch;
+    const int ti = u / ncw, ch = c0 + (u - ti * ncw);
     const int ky = KY0 + 2 * (ti / (NX > 0 ? NX : 1)), kx = KX0 + 2 * (ti % (NX > 0 ? NX : 1));
     return (size_t)(ky * KS + kx) * nch + ch;
   };
   // LDS entry of (tap, chunk) step u for this lane: fp32 entries are 4 channels, bf16 entries 8
   auto poff = [&](int u) -> int {
-    const int ti = u / nch, ch = u - ti * nch;
+    const int ti = u / ncw, ch = c0 + (u - ti * ncw);
     const int ky = KY0 + 2 * (ti / (NX > 0 ? NX : 1)), kx = KX0 + 2 * (ti % (NX > 0 ? NX : 1));
     const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
     return (BF ? (2 * ch + h) : (4 * ch + 2 * h)) * UP_PLANE + pr * UP_PC + pc;
@@ -842,20 +846,25 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
 }
 
 // --------------------------------------------------------------------------
-// Small-grid fp32 conv_up: the block owns ONE 32-pixel input tile (2 x 16) and wave w computes output-parity
-// class (w >> 1, w & 1) of it (9 / 6 / 6 / 4 taps).  Twice the blocks of conv_up_kernel (64-pixel tiles, two
-// classes per wave) and at most 9 instead of 13 taps of serial MFMA chain per wave: for the layers whose plain
-// grid leaves most CUs idle (the fine-tune's 256x256 crops: 16x16 .. 64x64 inputs, 32-512 blocks), which run at
-// the latency of one wave's K chain.  Same accumulation order per output element as conv_up_kernel.
+// Small-grid fp32 conv_up: a block computes ONE output-parity class (9 / 6 / 6 / 4 taps) of ONE 32-pixel input
+// tile (2 x 16), its 4 waves splitting the input-channel chunks (wave w: chunks [w nch / 4, (w + 1) nch / 4));
+// the partial accumulators are summed through LDS in wave order (deterministic) and wave 0 runs the epilogue.
+// 8x the blocks of conv_up_kernel (64-pixel tiles, two classes per wave) and 1/4-1/6 of its per-wave MFMA chain,
+// for the layers whose plain grid leaves most CUs idle (the fine-tune's 256x256 crops: 16x16 .. 64x64 inputs,
+// 32-512 blocks), where the plain kernel runs at the latency of one wave's K chain.
 // --------------------------------------------------------------------------
 constexpr int UPS_TH = 2, UPS_PLANE = (UPS_TH + 2) * UP_PC;
+template <int IT>
+constexpr int ups_red_entries() { return 3 * IT * 4 * 64; }   // partial sums of waves 1..3: [w-1][it][quad][lane]
 template <int KS, int IT, int EPI, int FX>
 __global__ __launch_bounds__(256, 2) void conv_up_small_kernel(ConvParams p) {
-  extern __shared__ f32x4 patch[];  // [Cin/4][UPS_TH + 2][UP_PC]
+  extern __shared__ f32x4 patch[];  // [Cin/4][UPS_TH + 2][UP_PC]; then reused for the partial sums
   const int Hh = p.Hin, Wh = p.Win;
   const int tiles_x = (Wh + UP_TW - 1) / UP_TW, tiles_y = (Hh + UPS_TH - 1) / UPS_TH;
   int bid, cb;
   xcd_block<true>(bid, cb);
+  const int cls = bid & 3;   // the 4 classes of a tile are neighbouring blocks (shared patch rows in L2)
+  bid >>= 2;
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
@@ -886,17 +895,40 @@ __global__ __launch_bounds__(256, 2) void conv_up_small_kernel(ConvParams p) {
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nch = p.Cin / 16;
+  const int lane = threadIdx.x & 63, c0 = wave * nch / 4, cn = (wave + 1) * nch / 4 - c0;
   auto run = [&](auto py_c, auto px_c) __attribute__((always_inline)) {
     constexpr int PY = decltype(py_c)::value, PX = decltype(px_c)::value;
     f32x16 acc[1][IT];
-    conv_up_acc<KS, PY, PX, IT, EPI, FX, false, UPS_TH>(p, patch, 0, cb, nch, acc);
+    conv_up_acc<KS, PY, PX, IT, EPI, FX, false, UPS_TH>(p, patch, 0, cb, nch, acc, c0, cn);   // cn >= 1 (host)
+    __syncthreads();   // every wave is done with the patch: its LDS now takes the partial sums
+    if (wave > 0) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          patch[(((wave - 1) * IT + it) * 4 + g) * 64 + lane] =
+              f32x4{acc[0][it][4 * g], acc[0][it][4 * g + 1], acc[0][it][4 * g + 2], acc[0][it][4 * g + 3]};
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll 1
+    for (int w = 0; w < 3; ++w) {   // one partial at a time (all 48 LDS reads hoisted spilled)
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 r = patch[((w * IT + it) * 4 + g) * 64 + lane];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[0][it][4 * g + e] += r[e];
+        }
+    }
     const int j = threadIdx.x & 31;
     const int oy = 2 * (a0 + (j >> 4)) + PY, ox = 2 * (b0 + (j & 15)) + PX;
     conv_epilogue<IT, EPI, FX, false>(p, acc[0], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  switch (wave) {
+  switch (cls) {
     case 0: run(I0{}, I0{}); break;
     case 1: run(I0{}, I1{}); break;
     case 2: run(I1{}, I0{}); break;
@@ -1435,8 +1467,8 @@ static int pick_down(const ConvParams& p, int KS, int S, int it, int epi, int fx
 template <int KS, int IT, int EPI, int FX>
 static int launch_up_small(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UPS_TH - 1) / UPS_TH) * p.N;
-  dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  const size_t lds = (size_t)(p.Cin / 4) * UPS_PLANE * sizeof(f32x4);
+  dim3 grid(4 * tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
+  const size_t lds = (size_t)std::max((p.Cin / 4) * UPS_PLANE, ups_red_entries<IT>()) * sizeof(f32x4);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1452,9 +1484,10 @@ static int launch_up_small(const ConvParams& p, hipStream_t st) {
 template <int KS, int IT, int EPI, int FX, bool BF = false>
 static int launch_up(const ConvParams& p, hipStream_t st) {
   if (p.Cin % 16 != 0 || p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win) return -2;
-  // small grids (inputs of at most 64 x 64 pixels per image): one class per wave over 32-pixel tiles
+  // small grids (inputs of at most 64 x 64 pixels per image): one class per block over 32-pixel tiles, the
+  // input-channel chunks split over the 4 waves (each needs one: Cin >= 64)
   if constexpr (!BF && KS == 5 && (FX == 0 || FX == FX_T) && (IT == 4 || IT == 6)) {
-    if (p.Hin * p.Win <= UP_SMALL_PX) return launch_up_small<KS, IT, EPI, FX>(p, st);
+    if (p.Hin * p.Win <= UP_SMALL_PX && p.Cin >= 64) return launch_up_small<KS, IT, EPI, FX>(p, st);
   }
   constexpr int UP_TH = up_th<BF>();
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
