@@ -38,6 +38,9 @@ __device__ unsigned long long ica_bf_trace[32768 * 4 * 8];
 extern "C" int ica_bf_trace_read(void* dst, size_t bytes) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ica_bf_trace), bytes, 0, hipMemcpyDeviceToHost);
 }
+extern "C" int ica_bf_trace_clear(const void* zeros, size_t bytes) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ica_bf_trace), zeros, bytes, 0, hipMemcpyHostToDevice);
+}
 #else
 #define BFT(k) \
   do {         \

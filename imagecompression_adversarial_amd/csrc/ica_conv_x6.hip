@@ -38,6 +38,9 @@ __device__ unsigned long long ica_x6_trace[32768 * 4 * 8];
 extern "C" int ica_x6_trace_read(void* dst, size_t bytes) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ica_x6_trace), bytes, 0, hipMemcpyDeviceToHost);
 }
+extern "C" int ica_x6_trace_clear(const void* zeros, size_t bytes) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ica_x6_trace), zeros, bytes, 0, hipMemcpyHostToDevice);
+}
 #else
 #define X6T(k) \
   do {         \

@@ -62,6 +62,7 @@ def run(names):
     }
     L = lib()
     L.ica_x6_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    L.ica_x6_trace_clear.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     buf = np.zeros(32768 * 4 * 8, dtype=np.uint64)  # first 32768 blocks
     for nm in names or list(cases):
         f = cases[nm]
@@ -69,6 +70,7 @@ def run(names):
             f()
         torch.cuda.synchronize()
         buf[:] = 0
+        assert L.ica_x6_trace_clear(buf.ctypes.data, buf.nbytes) == 0   # stamps of earlier cases must not survive
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         f()
