@@ -1,0 +1,113 @@
+"""GPU parity of the small-grid fp32 conv kernels (round 2): conv_down_split_kernel (k5 s2 conv_down,
+output <= 64x64 per image) and conv_up_small_kernel (k5 s2 conv_up, input <= 64x64 per image), each next to the
+plain kernel just past the threshold, with fused GDN / IGDN forward and backward epilogues, against the CPU oracle
+(autograd of the reference layer algebra, oracle/codec.py).  Tolerances (fp32, stated): rel-max <= 2e-5 of the
+tensor max for the forward layers, <= 5e-5 for the GDN-backward epilogues (as tests/test_gpu_kernels.py).  The
+kernel choice is per image, so a batch and its images run one at a time agree bit-for-bit."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import codec
+from tests.conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+C = 128
+
+
+def rnd(shape, seed, lo=-1.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g) * (hi - lo) + lo
+
+
+@pytest.fixture(scope="module")
+def K():
+    from imagecompression_adversarial_amd import hip_ops
+    return hip_ops
+
+
+def _gdn(seed):
+    P = codec.perturb_params(dict(zip(("a.beta", "a.gamma"), codec.gdn_init(C))), seed=seed)
+    return P["a.beta"], P["a.gamma"]
+
+
+# (H, W) of the GDN layer's output: conv_down out H x W (split kernel iff H W <= 4096), the next conv's
+# input-gradient conv_up reads H/2 x W/2 (small kernel iff (H/2)(W/2) <= 4096)
+@pytest.mark.parametrize("hw", [(64, 64), (66, 68), (132, 132), (16, 24)])
+def test_analysis_gdn_pair(K, hw):
+    """g_a layer pair: y = GDN(conv(x)) on conv_down + fused GDN (save), then d/d pre of conv(y) on conv_up + fused
+    GDN backward, vs autograd."""
+    H, W = hw
+    beta, gamma = _gdn(21)
+    gd = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
+    x0 = rnd((2, C, 2 * H, 2 * W), 22)
+    w0 = rnd((C, C, 5, 5), 23) * 0.02
+    b0 = rnd((C,), 24) * 0.1
+    w1 = rnd((C, C, 5, 5), 25) * 0.02
+    pre = F.conv2d(x0, w0, b0, stride=2, padding=2).requires_grad_(True)
+    y = codec.gdn(pre, beta, gamma, False)
+    z = F.conv2d(y, w1, None, stride=2, padding=2)
+    gz = rnd(tuple(z.shape), 26)
+    z.backward(gz)
+    p0 = K.PackedConv(w0.to(DEV), b0.to(DEV), "conv", 2)
+    p1 = K.PackedConv(w1.to(DEV), None, "conv", 2)
+    y4, sx, ss = K.conv_down(K.to_nc4(x0.to(DEV)), C, p0.fwd, p0.bias, C, 5, 2, K.EPI_GDN, gd, save=True)
+    assert rel_err(K.from_nc4(y4, C).cpu(), y.detach()) < 2e-5
+    dx4, _, _ = K.conv_up(K.to_nc4(gz.to(DEV)), C, p1.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(sx, ss))
+    dx = K.from_nc4(dx4, C).cpu()
+    assert rel_err(dx, pre.grad) < 5e-5
+    # per-image kernel choice: image 1 alone gives the same bits as in the batch
+    y4b, sxb, ssb = K.conv_down(K.to_nc4(x0[1:].to(DEV)), C, p0.fwd, p0.bias, C, 5, 2, K.EPI_GDN, gd, save=True)
+    assert torch.equal(y4b, y4[1:]) and torch.equal(ssb, ss[1:])
+    dx4b, _, _ = K.conv_up(K.to_nc4(gz[1:].to(DEV)), C, p1.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(sxb, ssb))
+    assert torch.equal(dx4b, dx4[1:])
+
+
+# (h, w) of the synthesis layer's input: conv_up in h x w (small kernel iff h w <= 4096); the next deconv's
+# input-gradient conv_down writes 2h x 2w (split kernel iff 4 h w <= 4096)
+@pytest.mark.parametrize("hw", [(16, 24), (32, 32), (33, 34), (66, 66)])
+def test_synthesis_igdn_pair(K, hw):
+    """g_s layer pair: y = IGDN(deconv(x)) on conv_up + fused IGDN (save), then d/d pre of deconv(y) on conv_down +
+    fused IGDN backward, vs autograd."""
+    h, w = hw
+    beta, gamma = _gdn(31)
+    gd = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
+    x0 = rnd((2, C, h, w), 32)
+    w0 = rnd((C, C, 5, 5), 33) * 0.02
+    b0 = rnd((C,), 34) * 0.1
+    w1 = rnd((C, C, 5, 5), 35) * 0.02
+    pre = F.conv_transpose2d(x0, w0, b0, stride=2, padding=2, output_padding=1).requires_grad_(True)
+    y = codec.gdn(pre, beta, gamma, True)
+    z = F.conv_transpose2d(y, w1, None, stride=2, padding=2, output_padding=1)
+    gz = rnd(tuple(z.shape), 36)
+    z.backward(gz)
+    p0 = K.PackedConv(w0.to(DEV), b0.to(DEV), "deconv", 2)
+    p1 = K.PackedConv(w1.to(DEV), None, "deconv", 2)
+    y4, sx, ss = K.conv_up(K.to_nc4(x0.to(DEV)), C, p0.fwd, p0.bias, C, K.EPI_IGDN, gd, save=True)
+    assert rel_err(K.from_nc4(y4, C).cpu(), y.detach()) < 2e-5
+    dx4, _, _ = K.conv_down(K.to_nc4(gz.to(DEV)), C, p1.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gd, saved=(sx, ss))
+    assert rel_err(K.from_nc4(dx4, C).cpu(), pre.grad) < 5e-5
+    y4b, sxb, ssb = K.conv_up(K.to_nc4(x0[:1].to(DEV)), C, p0.fwd, p0.bias, C, K.EPI_IGDN, gd, save=True)
+    assert torch.equal(y4b, y4[:1]) and torch.equal(ssb, ss[:1])
+
+
+@pytest.mark.parametrize("cout,hw", [(192, (16, 16)), (192, (32, 48)), (128, (40, 40))])
+def test_bias_layers(K, cout, hw):
+    """The plain-bias layers at the small sizes of the fine-tune crops (g_a.6 forward: 128 -> M, IT 3; the g_s.0
+    input gradient) and their input gradients, vs torch."""
+    H, W = hw
+    x = rnd((2, C, 2 * H, 2 * W), 41)
+    w = rnd((cout, C, 5, 5), 42) * (1.0 / (C * 25) ** 0.5)
+    b = rnd((cout,), 43) * 0.1
+    ref = F.conv2d(x, w, b, stride=2, padding=2)
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2)
+    y4, _, _ = K.conv_down(K.to_nc4(x.to(DEV)), C, p.fwd, p.bias, cout, 5, 2, K.EPI_BIAS)
+    assert rel_err(K.from_nc4(y4, cout).cpu(), ref) < 2e-5
+    # input gradient (conv_up from cout channels back to C)
+    xr = x.clone().requires_grad_(True)
+    yr = F.conv2d(xr, w, None, stride=2, padding=2)
+    g = rnd(tuple(yr.shape), 44)
+    yr.backward(g)
+    gx4, _, _ = K.conv_up(K.to_nc4(g.to(DEV)), cout, p.bwd, None, C)
+    assert rel_err(K.from_nc4(gx4, C).cpu(), xr.grad) < 2e-5
