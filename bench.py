@@ -35,8 +35,9 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA, dense (no
 
 
 def layer_flops(tag, N, M, H, W, B):
-    """Algorithmic FLOPs of one launch of a tagged conv kernel (2*MAC, padding not counted)."""
-    name, kind = tag.rsplit(".", 1)
+    """Algorithmic FLOPs of one launch of a tagged conv kernel (2*MAC, padding not counted).  A '[prec]' suffix
+    (hip_ops: the same layer run on other operands, e.g. the fine-tune's fp32 train step) does the same work."""
+    name, kind = tag.split("[", 1)[0].rsplit(".", 1)
     lay = {  # (conv type, Cin, Cout, output resolution divisor, gdn channels in epilogue)
         "g_a.0": ("down", 3, N, 2, N), "g_a.2": ("down", N, N, 4, N), "g_a.4": ("down", N, N, 8, N),
         "g_a.6": ("down", N, M, 16, 0),

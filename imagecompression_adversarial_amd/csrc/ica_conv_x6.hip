@@ -53,14 +53,20 @@ namespace {
 #define X6_PF 1   // conv_down_x6 patch prefetch: 0 none, 1 first batch during the previous chunk, 2 both batches
 #endif
 constexpr int X6_PT = 2;                 // 32-pixel tiles per wave
-constexpr int XD_TW = 32, XD_TH = 4 * X6_PT;
+constexpr int XD_TW = 32;
+// conv_down_x6 rows per block: 4 waves x PT tiles of one 32-pixel row each.  PT = 1 (128-pixel blocks, 71 KB of LDS)
+// for outputs of at most 64 x 64 pixels per image, whose PT = 2 grid (256-pixel blocks, one per CU) would leave CUs
+// idle (the fine-tune's 64 x 64 layers: 128 blocks for 256 CUs).  Both run the same MFMA sequence per output.
+template <int PT>
+constexpr int xd_th() { return 4 * PT; }
+constexpr int XD_SMALL_PX = 64 * 64;
 
 // --------------------------------------------------------------------------------------------------------------
 // conv_down_x6: weights [plane][cb][chunk][tap][it][lane] bf16x8 (plane stride ps fragments)
 // --------------------------------------------------------------------------------------------------------------
-template <int IT, int EPI>
+template <int IT, int EPI, int PT = X6_PT>
 __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long ps) {
-  constexpr int KS = 5, S = 2, PAD = 2, KK = 25, PT = X6_PT, TW = XD_TW, TH = XD_TH;
+  constexpr int KS = 5, S = 2, PAD = 2, KK = 25, TW = XD_TW, TH = xd_th<PT>();
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;
   constexpr int NF = (4 * PLANE + 255) / 256, NB = (NF + 1) / 2;  // fill items per thread, in two batches
   __shared__ f32x4 patch[3 * 2 * PLANE];                          // [plane][half][pixel]: 8 channels as bf16
@@ -499,14 +505,21 @@ __global__ void pack_gdn_x6_kernel(const float* __restrict__ gp, __bf16* __restr
   dst[2 * total + i] = (__bf16)(r1 - (float)b);
 }
 
-template <int IT, int EPI>
-int launch_down_x6(const ConvParams& p, hipStream_t st) {
-  const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + XD_TH - 1) / XD_TH) * p.N;
+template <int IT, int EPI, int PT>
+int launch_down_x6_pt(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + xd_th<PT>() - 1) / xd_th<PT>()) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * ((((p.Cin + 3) / 4) * 4 + 15) / 16) * 25 * IT * 64;
-  hipLaunchKernelGGL((conv_down_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+  hipLaunchKernelGGL((conv_down_x6_kernel<IT, EPI, PT>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
+}
+
+// a per-image rule (output pixels per image), so image b of a batch runs the same kernel at any batch size
+template <int IT, int EPI>
+int launch_down_x6(const ConvParams& p, hipStream_t st) {
+  if (p.Hout * p.Wout <= XD_SMALL_PX) return launch_down_x6_pt<IT, EPI, 1>(p, st);
+  return launch_down_x6_pt<IT, EPI, X6_PT>(p, st);
 }
 
 template <int IT, int EPI>

@@ -47,9 +47,19 @@ def _ev_end(h, flops=None):
 PREC_HOOK = {}
 
 
+_PREC_SUFFIX = {0: "fp32", 1: "bf16", 2: "x6"}   # PREC_FP32, PREC_BF16, PREC_X6
+
+
 def _prec_note(tag, prec):
-    if EVENT_HOOK is not None and tag is not None:
-        PREC_HOOK[tag] = prec
+    """Record the operands a tagged launch runs on; returns the tag to time it under: a tag first seen with other
+    operands (e.g. the fine-tune's fp32 train step next to its x6 inner attack) is timed as 'tag[fp32]'."""
+    if EVENT_HOOK is None or tag is None:
+        return tag
+    first = PREC_HOOK.setdefault(tag, prec)
+    if first != prec:
+        tag = f"{tag}[{_PREC_SUFFIX.get(prec, prec)}]"
+        PREC_HOOK.setdefault(tag, prec)
+    return tag
 
 
 # algorithmic FLOPs PER IMAGE of each tagged ica_conv_ex launch (filled while EVENT_HOOK is set): 2*MAC of the
@@ -372,7 +382,7 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
     prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex).
     it: the row-tile count wp was packed with (0 = library default; explicit values go through ica_conv_ex)."""
     N, _, H, W, _ = x4.shape
-    _prec_note(tag, prec)
+    tag = _prec_note(tag, prec)
     if prec in (PREC_BF16, PREC_X6) or it:
         return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
@@ -398,7 +408,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
             out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
     """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
     N, _, H, W, _ = x4.shape
-    _prec_note(tag, prec)
+    tag = _prec_note(tag, prec)
     if (prec in (PREC_BF16, PREC_X6) or it) and Cout != 3:
         return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t, prec, it)
     Ho, Wo = 2 * H, 2 * W
