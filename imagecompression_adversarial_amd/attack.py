@@ -159,6 +159,13 @@ class AttackLoop:
         self.sel = torch.zeros(B + 1, dtype=torch.int32, device=dev)
         self.gpos = torch.zeros(B, dtype=torch.int32, device=dev)
         self.sel_host = torch.zeros(B + 1, dtype=torch.int32).pin_memory() if dev.type == "cuda" else None
+        # speculation: after a step whose images were all on the expensive branch, the next step runs the network on
+        # the whole batch without waiting for its own selection (read one step later, when the GPU still has that
+        # step's network work queued).  The Adam kernel takes each image's branch from the device, and an image's
+        # gradient does not depend on the batch it runs in, so the results are the same bits either way; a cheap
+        # image costs one step of unused network work.
+        self._sel_ev = torch.cuda.Event() if dev.type == "cuda" else None
+        self._sel_pending = False
         self.census = torch.zeros(B, dtype=torch.int32, device=dev)
         self.steps_done = 0
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
@@ -193,10 +200,21 @@ class AttackLoop:
         if not self.compact:
             return B, None
         call("ica_branch_select", ptr(self.loss_i), self.thr, B, ptr(self.sel), ptr(self.gpos), stream())
+        prev_all = False
+        if self._sel_pending:   # the previous step's selection (its copy was queued one step ago)
+            self._sel_ev.synchronize()
+            prev_all = int(self.sel_host[0]) == B
+            self._sel_pending = False
         self.sel_host.copy_(self.sel, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
+        self._sel_ev.record()
+        # (ms-ssim needs the host to know whether any image is cheap: its cheap-branch gradient is a separate launch)
+        if prev_all and (self.metric == "L2" or self.roi is not None):   # speculate: the whole batch, no wait
+            self._sel_pending = True
+            return B, None
+        self._sel_ev.synchronize()
         E = int(self.sel_host[0])
         if E == B:
+            self._sel_pending = True   # (already complete) lets the next step speculate
             return B, None
         return E, self.sel[1:1 + E]
 
