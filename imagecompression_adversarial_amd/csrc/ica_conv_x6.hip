@@ -21,6 +21,7 @@
 //                  pixels (16 x 32 outputs); the channel group (all of Cin, or 64-channel groups) lives in LDS;
 //                  each wave runs two classes (9 + 4 or 6 + 6 taps) over 2 pixel tiles.
 // One block per CU (the 3-plane patches take 122 / 138 KB of LDS), so each wave has the whole 512-register file.
+#include <algorithm>
 #include <type_traits>
 
 #include "ica_conv_epi.h"
@@ -55,11 +56,10 @@ namespace {
 constexpr int X6_PT = 2;                 // 32-pixel tiles per wave
 constexpr int XD_TW = 32;
 // conv_down_x6 rows per block: 4 waves x PT tiles of one 32-pixel row each.  PT = 1 (128-pixel blocks, 71 KB of LDS)
-// for outputs of at most 64 x 64 pixels per image, whose PT = 2 grid (256-pixel blocks, one per CU) would leave CUs
-// idle (the fine-tune's 64 x 64 layers: 128 blocks for 256 CUs).  Both run the same MFMA sequence per output.
+// where the PT = 2 grid (256-pixel blocks, one per CU) would leave CUs idle (the fine-tune's 64 x 64 layers: 128
+// blocks for 256 CUs).  Both run the same MFMA sequence per output.
 template <int PT>
 constexpr int xd_th() { return 4 * PT; }
-constexpr int XD_SMALL_PX = 64 * 64;
 
 // --------------------------------------------------------------------------------------------------------------
 // conv_down_x6: weights [plane][cb][chunk][tap][it][lane] bf16x8 (plane stride ps fragments)
@@ -460,6 +460,258 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
   }
 }
 
+// --------------------------------------------------------------------------------------------------------------
+// Small-grid x6 kernels (layers whose low-resolution side is <= 32 x 32 per image: the fine-tune's 256x256 crops).
+// The structure of the fp32 small-grid kernels of ica_conv.hip on x6 operands: a 32-pixel tile per
+// block, the K loop split over the 4 waves, partial sums reduced through LDS in wave order (deterministic), wave 0
+// runs the (narrow) x6 epilogue.  Six 32-cycle bf16 MFMAs per 16-deep k step instead of eight 64-cycle fp32 ones:
+// the per-wave chain that bounds these latency-bound launches is 2.7x shorter.
+// --------------------------------------------------------------------------------------------------------------
+constexpr int XSD_TW = 8, XSD_TH = 4;   // conv_down: 4 x 8 output pixels per block
+template <int IT>
+constexpr int xs_red_entries() { return 3 * IT * 4 * 64; }
+
+// partial sums of waves 1..3 into red, wave 0 adds them in wave order; returns true on wave 0
+template <int IT>
+ICA_DEV bool xs_reduce(f32x16 (&acc)[IT], f32x4* red, int wave, int lane) {
+  if (wave > 0) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        red[(((wave - 1) * IT + it) * 4 + g) * 64 + lane] =
+            f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]};
+  }
+  __syncthreads();
+  if (wave != 0) return false;
+#pragma unroll 1
+  for (int w = 0; w < 3; ++w) {   // one partial at a time (hoisting every LDS read spilled)
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 r = red[((w * IT + it) * 4 + g) * 64 + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += r[e];
+      }
+  }
+  return true;
+}
+
+// conv_down (k5 s2): the 4 waves share one 4 x 8 output tile and split its 25 taps
+template <int IT, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_down_small_x6_kernel(ConvParams p, long ps) {
+  constexpr int KS = 5, S = 2, PAD = 2, KK = 25, TW = XSD_TW, TH = XSD_TH;
+  constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;   // 11 x 19
+  constexpr int NF = (4 * PLANE + 255) / 256;
+  __shared__ f32x4 patch[3 * 2 * PLANE];   // [plane][half][pixel]: 8 channels as bf16
+  __shared__ f32x4 red[xs_red_entries<IT>()];
+  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5,
+            j = lane & 31;
+  const int oy0 = ty * TH, ox0 = tx * TW, iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int Cin4 = (p.Cin + 3) >> 2, nch = (Cin4 * 4 + 15) / 16;
+  const int oyl = j / TW, oxl = j % TW, lbase = S * oyl * PC + S * oxl;
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  auto fill = [&](int ch) {
+    f32x4 v[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+      const int iy = iy0 + pr, ix = ix0 + pc, c4 = ch * 4 + q;
+      const bool ok = e < 4 * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e < 4 * PLANE) {
+        const int q = e / PLANE, pix = e - q * PLANE;
+        u32x2 a, b, c;
+        split3(v[i], a, b, c);
+        const int ent = (q >> 1) * PLANE + pix;
+        p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
+        p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+        p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+      }
+    }
+    __syncthreads();
+  };
+  const int t0 = wave * KK / 4, nt = (wave + 1) * KK / 4 - t0, total = nch * nt;
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * nch * KK * IT * 64;
+  auto ldw = [&](bf16x8 (&a)[IT][3], int u) {
+    u = min(u, total - 1);
+    const int ch = u / nt, tap = t0 + (u - ch * nt);
+    const int f = wbase + (ch * KK + tap) * IT * 64;
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+  };
+  f32x16 acc[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int u) __attribute__((always_inline)) {
+    ldw(nxt, u + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const int ch = u / nt, tap = t0 + (u - ch * nt);
+    const int ky = tap / KS, kx = tap - ky * KS;
+    const int o = h * PLANE + lbase + ky * PC + kx;
+    const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[it] = mfma_x6(cur[it], b, acc[it]);
+  };
+  bf16x8 fa[IT][3], fb[IT][3];
+  ldw(fa, 0);
+  int u = 0;
+#pragma unroll 1
+  for (int ch = 0; ch < nch; ++ch) {
+    fill(ch);   // every wave joins every chunk's barriers
+    const int ue = u + nt;
+#pragma unroll 1
+    for (; u + 1 < ue; u += 2) {
+      step(fa, fb, u);
+      step(fb, fa, u + 1);
+    }
+    if (u < ue) {   // odd step count: the prefetched set moves to fa (once per chunk)
+      step(fa, fb, u);
+      ++u;
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) fa[it][q] = fb[it][q];
+    }
+  }
+  if (!xs_reduce<IT>(acc, red, wave, lane)) return;
+  const int oy = oy0 + oyl, ox = ox0 + oxl;
+  conv_epilogue<IT, EPI, 0, false, 2>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+}
+
+// conv_up (k5 s2 p2 op1): one block = one output-parity class of one 2 x 16 input tile, the input-channel chunks
+// split over the 4 waves; the whole-Cin patch as three bf16 planes
+constexpr int XSU_TH = 2, XSU_PC = 18, XSU_PLANE = (XSU_TH + 2) * XSU_PC;   // 72 pixels
+template <int IT, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_up_small_x6_kernel(ConvParams p, long ps) {
+  constexpr int KS = 5, PAD = 2, TW = 16;
+  extern __shared__ f32x4 patch[];   // [plane][Cin/8][XSU_PLANE]; then the partial sums
+  const int tiles_x = (p.Win + TW - 1) / TW, tiles_y = (p.Hin + XSU_TH - 1) / XSU_TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int cls = bid & 3;
+  bid >>= 2;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int a0 = ty * XSU_TH, b0 = tx * TW;
+  const int Cin4 = p.Cin >> 2, nch = p.Cin / 16, NQ8 = p.Cin / 8;
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  {
+    constexpr int FB = 8;
+    const int TOT = Cin4 * XSU_PLANE;
+    for (int e0 = threadIdx.x; e0 < TOT; e0 += 256 * FB) {
+      f32x4 v[FB];
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        const int e = e0 + 256 * i;
+        const int q = e / XSU_PLANE, rem = e - q * XSU_PLANE, pr = rem / XSU_PC, pc = rem - pr * XSU_PC;
+        const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+        const bool ok = e < TOT && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+        const unsigned vo = ((unsigned)q * xplane + (unsigned)iy * p.Win + ix) * 16u;
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        const int e = e0 + 256 * i;
+        if (e < TOT) {
+          const int q = e / XSU_PLANE, pix = e - q * XSU_PLANE;
+          u32x2 a, b, c;
+          split3(v[i], a, b, c);
+          const int ent = (q >> 1) * XSU_PLANE + pix;
+          p2[(0 * NQ8 * XSU_PLANE + ent) * 2 + (q & 1)] = a;
+          p2[(1 * NQ8 * XSU_PLANE + ent) * 2 + (q & 1)] = b;
+          p2[(2 * NQ8 * XSU_PLANE + ent) * 2 + (q & 1)] = c;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5,
+            j = lane & 31;
+  const int c0 = wave * nch / 4, cn = (wave + 1) * nch / 4 - c0;   // cn >= 1: Cin >= 64 (host)
+  const int a_rel = j >> 4, b_rel = j & 15;
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * KS * KS * nch * IT * 64;
+  auto run = [&](auto py_c, auto px_c) __attribute__((always_inline)) {
+    constexpr int PY = decltype(py_c)::value, PX = decltype(px_c)::value;
+    constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
+    constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
+    const int total = NT * cn;
+    auto ldw = [&](bf16x8 (&a)[IT][3], int u) {
+      u = min(u, total - 1);
+      const int ti = u / cn, c = c0 + (u - ti * cn);
+      const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+      const int f = wbase + ((ky * KS + kx) * nch + c) * IT * 64;
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+    };
+    f32x16 acc[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+    auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int u) __attribute__((always_inline)) {
+      ldw(nxt, u + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int ti = u / cn, c = c0 + (u - ti * cn);
+      const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+      const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
+      const int o = (2 * c + h) * XSU_PLANE + pr * XSU_PC + pc;
+      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[NQ8 * XSU_PLANE + o]),
+                           f4_as_bf8(patch[2 * NQ8 * XSU_PLANE + o])};
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[it] = mfma_x6(cur[it], b, acc[it]);
+    };
+    bf16x8 fa[IT][3], fb[IT][3];
+    ldw(fa, 0);
+    int u = 0;
+#pragma unroll 1
+    for (; u + 1 < total; u += 2) {
+      step(fa, fb, u);
+      step(fb, fa, u + 1);
+    }
+    if (u < total) step(fa, fb, u);
+    __syncthreads();   // every wave is done with the patch: its LDS takes the partial sums
+    if (!xs_reduce<IT>(acc, patch, wave, lane)) return;
+    const int oy = 2 * (a0 + a_rel) + PY, ox = 2 * (b0 + b_rel) + PX;
+    conv_epilogue<IT, EPI, 0, false, 2>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  switch (cls) {
+    case 0: run(I0{}, I0{}); break;
+    case 1: run(I0{}, I1{}); break;
+    case 2: run(I1{}, I0{}); break;
+    default: run(I1{}, I1{}); break;
+  }
+}
+
 // (cb, outer, inner, it, lane, s) fragment index of pack_conv_kernel (CC = 16) -> three split planes
 __global__ void pack_conv_x6_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int O, int C, int KS,
                                     long so, long sc, int IT, int order, long total) {
@@ -515,10 +767,28 @@ int launch_down_x6_pt(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
-// a per-image rule (output pixels per image), so image b of a batch runs the same kernel at any batch size
+constexpr int XS_SMALL_PX = 32 * 32;   // the small-grid x6 kernels: low-resolution side <= 32 x 32 per image
+
+template <int IT, int EPI>
+int launch_down_small_x6(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Wout + XSD_TW - 1) / XSD_TW) * ((p.Hout + XSD_TH - 1) / XSD_TH) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * ((((p.Cin + 3) / 4) * 4 + 15) / 16) * 25 * IT * 64;
+  hipLaunchKernelGGL((conv_down_small_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Small grids (<= 32 x 32 outputs per image, a per-image rule: image b of a batch runs the same kernel at any
+// batch size) take the small-grid kernel.  Otherwise PT = 1 when the PT = 2 grid would leave CUs idle (fewer
+// blocks than the 256 CUs): PT = 1 and PT = 2 run the same MFMA and epilogue sequence per output (same bits), so
+// this batch-dependent choice keeps every image's result.
 template <int IT, int EPI>
 int launch_down_x6(const ConvParams& p, hipStream_t st) {
-  if (p.Hout * p.Wout <= XD_SMALL_PX) return launch_down_x6_pt<IT, EPI, 1>(p, st);
+  if (p.Hout * p.Wout <= XS_SMALL_PX) return launch_down_small_x6<IT, EPI>(p, st);
+  const int blocks2 = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + xd_th<X6_PT>() - 1) / xd_th<X6_PT>()) * p.N *
+                      ((p.Cout + IT * 32 - 1) / (IT * 32));
+  if (blocks2 < 256) return launch_down_x6_pt<IT, EPI, 1>(p, st);
   return launch_down_x6_pt<IT, EPI, X6_PT>(p, st);
 }
 
@@ -551,7 +821,26 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
 }
 
 template <int IT, int EPI>
+int launch_up_small_x6(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Win + 15) / 16) * ((p.Hin + XSU_TH - 1) / XSU_TH) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * 25 * (p.Cin / 16) * IT * 64;
+  const size_t lds = (size_t)std::max(3 * (p.Cin / 8) * XSU_PLANE, xs_red_entries<IT>()) * 16;
+  if (lds > 160 * 1024) return -2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_small_x6_kernel<IT, EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_up_small_x6_kernel<IT, EPI>), dim3(4 * tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int IT, int EPI>
 int pick_up_x6(const ConvParams& p, hipStream_t st) {
+  if (p.Hin * p.Win <= XS_SMALL_PX && p.Cin >= 64 && p.Cin % 16 == 0) return launch_up_small_x6<IT, EPI>(p, st);
   if (p.Cin <= 128 && p.Cin % 16 == 0) {
     if (p.Cin == 128) return launch_up_x6<IT, EPI, 128>(p, st);
     if (p.Cin == 64) return launch_up_x6<IT, EPI, 64>(p, st);

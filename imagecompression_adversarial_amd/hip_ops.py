@@ -278,8 +278,6 @@ class PackedConv:
         keep the fp32 packs."""
         fp = PackedConv(weight, bias, kind, stride, PREC_FP32, self.it_fwd, self.it_bwd)
         self.__dict__.update(fp.__dict__)
-        # the fp32 packs stay: small grids (sel_fwd / sel_bwd) run the fp32 small-grid kernels
-        self.fwd32, self.bwd32 = fp.fwd, fp.bwd
         if self.KS != 5 or stride != 2:
             return
         KK = 25
@@ -312,22 +310,15 @@ class PackedConv:
                 self.bwd_prec = PREC_X6
 
 
-    # x6 launches whose low-resolution side (conv_down output / conv_up input) has at most X6_SMALL_PX pixels per
-    # image run the fp32 small-grid kernels instead (conv_down_split_kernel / conv_up_small_kernel, fp32 MFMA): an
-    # x6 block covers 256 pixels at one block per CU, so such layers (the fine-tune's 256x256 crops below 64x64)
-    # would leave most CUs idle.  A per-image rule: image b of a batch runs the same kernels at any batch size.
-    X6_SMALL_PX = 32 * 32
-
+    # The pack a launch uses (one place to choose; lowres_px = pixels per image of the layer's low-resolution side).
+    # x6 layers of any size stay on x6 operands: the library dispatches small grids (<= 32 x 32 per image) to its
+    # small-grid x6 kernels and 33x33..64x64 conv_down outputs to 128-pixel blocks.
     def sel_fwd(self, lowres_px: int):
-        """(pack, prec) of the forward launch for a layer whose low-resolution side has lowres_px pixels."""
-        if self.fwd_prec == PREC_X6 and lowres_px <= self.X6_SMALL_PX and getattr(self, "fwd32", None) is not None:
-            return self.fwd32, PREC_FP32
+        """(pack, prec) of the forward launch."""
         return self.fwd, self.fwd_prec
 
     def sel_bwd(self, lowres_px: int):
-        """(pack, prec) of the input-gradient launch (see sel_fwd)."""
-        if self.bwd_prec == PREC_X6 and lowres_px <= self.X6_SMALL_PX and getattr(self, "bwd32", None) is not None:
-            return self.bwd32, PREC_FP32
+        """(pack, prec) of the input-gradient launch."""
         return self.bwd, self.bwd_prec
 
 

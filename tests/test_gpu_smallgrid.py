@@ -1,6 +1,8 @@
-"""GPU parity of the small-grid fp32 conv kernels (round 2): conv_down_split_kernel (k5 s2 conv_down,
-output <= 64x64 per image) and conv_up_small_kernel (k5 s2 conv_up, input <= 64x64 per image), each next to the
-plain kernel just past the threshold, with fused GDN / IGDN forward and backward epilogues, against the CPU oracle
+"""GPU parity of the small-grid conv kernels (round 2): fp32 operands (conv_down_split_kernel, k5 s2
+conv_down with output <= 64x64 per image; conv_up_small_kernel, input <= 64x64 per image) and x6 operands
+(conv_down_small_x6 / conv_up_small_x6 at <= 32x32, conv_down_x6 PT = 1 where the PT = 2 grid has < 256 blocks),
+each next to the plain
+kernel just past its threshold, with fused GDN / IGDN forward and backward epilogues, against the CPU oracle
 (autograd of the reference layer algebra, oracle/codec.py).  Tolerances (fp32, stated): rel-max <= 2e-5 of the
 tensor max for the forward layers, <= 5e-5 for the GDN-backward epilogues (as tests/test_gpu_kernels.py).  The
 kernel choice is per image, so a batch and its images run one at a time agree bit-for-bit."""
@@ -34,8 +36,9 @@ def _gdn(seed):
 
 # (H, W) of the GDN layer's output: conv_down out H x W (split kernel iff H W <= 4096), the next conv's
 # input-gradient conv_up reads H/2 x W/2 (small kernel iff (H/2)(W/2) <= 4096)
-@pytest.mark.parametrize("hw", [(64, 64), (66, 68), (132, 132), (16, 24)])
-def test_analysis_gdn_pair(K, hw):
+@pytest.mark.parametrize("prec", ["fp32", "x6"])
+@pytest.mark.parametrize("hw", [(64, 64), (66, 68), (132, 132), (16, 24), (32, 32)])
+def test_analysis_gdn_pair(K, hw, prec):
     """g_a layer pair: y = GDN(conv(x)) on conv_down + fused GDN (save), then d/d pre of conv(y) on conv_up + fused
     GDN backward, vs autograd."""
     H, W = hw
@@ -50,24 +53,55 @@ def test_analysis_gdn_pair(K, hw):
     z = F.conv2d(y, w1, None, stride=2, padding=2)
     gz = rnd(tuple(z.shape), 26)
     z.backward(gz)
-    p0 = K.PackedConv(w0.to(DEV), b0.to(DEV), "conv", 2)
-    p1 = K.PackedConv(w1.to(DEV), None, "conv", 2)
-    y4, sx, ss = K.conv_down(K.to_nc4(x0.to(DEV)), C, p0.fwd, p0.bias, C, 5, 2, K.EPI_GDN, gd, save=True)
+    pr = K.PREC_X6 if prec == "x6" else K.PREC_FP32
+    p0 = K.PackedConv(w0.to(DEV), b0.to(DEV), "conv", 2, pr)
+    p1 = K.PackedConv(w1.to(DEV), None, "conv", 2, pr)
+    assert p0.fwd_prec == pr and p1.bwd_prec == pr
+    y4, sx, ss = K.conv_down(K.to_nc4(x0.to(DEV)), C, p0.fwd, p0.bias, C, 5, 2, K.EPI_GDN, gd, save=True,
+                             prec=p0.fwd_prec)
     assert rel_err(K.from_nc4(y4, C).cpu(), y.detach()) < 2e-5
-    dx4, _, _ = K.conv_up(K.to_nc4(gz.to(DEV)), C, p1.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(sx, ss))
+    dx4, _, _ = K.conv_up(K.to_nc4(gz.to(DEV)), C, p1.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(sx, ss),
+                          prec=p1.bwd_prec)
     dx = K.from_nc4(dx4, C).cpu()
     assert rel_err(dx, pre.grad) < 5e-5
     # per-image kernel choice: image 1 alone gives the same bits as in the batch
-    y4b, sxb, ssb = K.conv_down(K.to_nc4(x0[1:].to(DEV)), C, p0.fwd, p0.bias, C, 5, 2, K.EPI_GDN, gd, save=True)
+    y4b, sxb, ssb = K.conv_down(K.to_nc4(x0[1:].to(DEV)), C, p0.fwd, p0.bias, C, 5, 2, K.EPI_GDN, gd, save=True,
+                                prec=p0.fwd_prec)
     assert torch.equal(y4b, y4[1:]) and torch.equal(ssb, ss[1:])
-    dx4b, _, _ = K.conv_up(K.to_nc4(gz[1:].to(DEV)), C, p1.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(sxb, ssb))
+    dx4b, _, _ = K.conv_up(K.to_nc4(gz[1:].to(DEV)), C, p1.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(sxb, ssb),
+                           prec=p1.bwd_prec)
     assert torch.equal(dx4b, dx4[1:])
+
+
+@pytest.mark.parametrize("B,hw", [(22, (48, 64)), (16, (64, 64))])
+def test_x6_down_pt1_same_bits(K, B, hw):
+    """conv_down_x6 picks PT = 1 (128-pixel blocks) for a grid of < 256 PT = 2 blocks and PT = 2 otherwise: a batch
+    (>= 256 PT = 2 blocks here: PT = 2) and its first image alone (PT = 1) give the same bits, for the GDN forward
+    and the IGDN-backward epilogues."""
+    H, W = hw
+    assert ((W + 31) // 32) * ((H + 7) // 8) * B >= 256 > ((W + 31) // 32) * ((H + 7) // 8)
+    beta, gamma = _gdn(51)
+    gd = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
+    x = rnd((B, C, 2 * H, 2 * W), 52).to(DEV)
+    w = rnd((C, C, 5, 5), 53) * 0.02
+    b = rnd((C,), 54) * 0.1
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2, K.PREC_X6)
+    y8, _, s8 = K.conv_down(K.to_nc4(x), C, p.fwd, p.bias, C, 5, 2, K.EPI_GDN, gd, save=True, prec=p.fwd_prec)
+    y1, _, s1 = K.conv_down(K.to_nc4(x[:1]), C, p.fwd, p.bias, C, 5, 2, K.EPI_GDN, gd, save=True, prec=p.fwd_prec)
+    assert torch.equal(y1, y8[:1]) and torch.equal(s1, s8[:1])
+    pd = K.PackedConv(w.to(DEV), None, "deconv", 2, K.PREC_X6)
+    g8, _, _ = K.conv_down(K.to_nc4(x), C, pd.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gd, saved=(y8, s8),
+                           prec=pd.bwd_prec)
+    g1, _, _ = K.conv_down(K.to_nc4(x[:1]), C, pd.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gd, saved=(y1, s1),
+                           prec=pd.bwd_prec)
+    assert torch.equal(g1, g8[:1])
 
 
 # (h, w) of the synthesis layer's input: conv_up in h x w (small kernel iff h w <= 4096); the next deconv's
 # input-gradient conv_down writes 2h x 2w (split kernel iff 4 h w <= 4096)
+@pytest.mark.parametrize("prec", ["fp32", "x6"])
 @pytest.mark.parametrize("hw", [(16, 24), (32, 32), (33, 34), (66, 66)])
-def test_synthesis_igdn_pair(K, hw):
+def test_synthesis_igdn_pair(K, hw, prec):
     """g_s layer pair: y = IGDN(deconv(x)) on conv_up + fused IGDN (save), then d/d pre of deconv(y) on conv_down +
     fused IGDN backward, vs autograd."""
     h, w = hw
@@ -82,18 +116,23 @@ def test_synthesis_igdn_pair(K, hw):
     z = F.conv_transpose2d(y, w1, None, stride=2, padding=2, output_padding=1)
     gz = rnd(tuple(z.shape), 36)
     z.backward(gz)
-    p0 = K.PackedConv(w0.to(DEV), b0.to(DEV), "deconv", 2)
-    p1 = K.PackedConv(w1.to(DEV), None, "deconv", 2)
-    y4, sx, ss = K.conv_up(K.to_nc4(x0.to(DEV)), C, p0.fwd, p0.bias, C, K.EPI_IGDN, gd, save=True)
+    pr = K.PREC_X6 if prec == "x6" else K.PREC_FP32
+    p0 = K.PackedConv(w0.to(DEV), b0.to(DEV), "deconv", 2, pr)
+    p1 = K.PackedConv(w1.to(DEV), None, "deconv", 2, pr)
+    assert p0.fwd_prec == pr and p1.bwd_prec == pr
+    y4, sx, ss = K.conv_up(K.to_nc4(x0.to(DEV)), C, p0.fwd, p0.bias, C, K.EPI_IGDN, gd, save=True, prec=p0.fwd_prec)
     assert rel_err(K.from_nc4(y4, C).cpu(), y.detach()) < 2e-5
-    dx4, _, _ = K.conv_down(K.to_nc4(gz.to(DEV)), C, p1.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gd, saved=(sx, ss))
+    dx4, _, _ = K.conv_down(K.to_nc4(gz.to(DEV)), C, p1.bwd, None, C, 5, 2, K.EPI_IGDN_BWD, gd, saved=(sx, ss),
+                            prec=p1.bwd_prec)
     assert rel_err(K.from_nc4(dx4, C).cpu(), pre.grad) < 5e-5
-    y4b, sxb, ssb = K.conv_up(K.to_nc4(x0[:1].to(DEV)), C, p0.fwd, p0.bias, C, K.EPI_IGDN, gd, save=True)
+    y4b, sxb, ssb = K.conv_up(K.to_nc4(x0[:1].to(DEV)), C, p0.fwd, p0.bias, C, K.EPI_IGDN, gd, save=True,
+                              prec=p0.fwd_prec)
     assert torch.equal(y4b, y4[:1]) and torch.equal(ssb, ss[:1])
 
 
+@pytest.mark.parametrize("prec", ["fp32", "x6"])
 @pytest.mark.parametrize("cout,hw", [(192, (16, 16)), (192, (32, 48)), (128, (40, 40))])
-def test_bias_layers(K, cout, hw):
+def test_bias_layers(K, cout, hw, prec):
     """The plain-bias layers at the small sizes of the fine-tune crops (g_a.6 forward: 128 -> M, IT 3; the g_s.0
     input gradient) and their input gradients, vs torch."""
     H, W = hw
@@ -101,13 +140,13 @@ def test_bias_layers(K, cout, hw):
     w = rnd((cout, C, 5, 5), 42) * (1.0 / (C * 25) ** 0.5)
     b = rnd((cout,), 43) * 0.1
     ref = F.conv2d(x, w, b, stride=2, padding=2)
-    p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2)
-    y4, _, _ = K.conv_down(K.to_nc4(x.to(DEV)), C, p.fwd, p.bias, cout, 5, 2, K.EPI_BIAS)
+    p = K.PackedConv(w.to(DEV), b.to(DEV), "conv", 2, K.PREC_X6 if prec == "x6" else K.PREC_FP32)
+    y4, _, _ = K.conv_down(K.to_nc4(x.to(DEV)), C, p.fwd, p.bias, cout, 5, 2, K.EPI_BIAS, prec=p.fwd_prec)
     assert rel_err(K.from_nc4(y4, cout).cpu(), ref) < 2e-5
     # input gradient (conv_up from cout channels back to C)
     xr = x.clone().requires_grad_(True)
     yr = F.conv2d(xr, w, None, stride=2, padding=2)
     g = rnd(tuple(yr.shape), 44)
     yr.backward(g)
-    gx4, _, _ = K.conv_up(K.to_nc4(g.to(DEV)), cout, p.bwd, None, C)
+    gx4, _, _ = K.conv_up(K.to_nc4(g.to(DEV)), cout, p.bwd, None, C, prec=p.bwd_prec)
     assert rel_err(K.from_nc4(gx4, C).cpu(), xr.grad) < 2e-5
