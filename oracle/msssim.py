@@ -5,7 +5,9 @@ TEST INFRASTRUCTURE (see oracle/__init__.py).
 (i)  ``ms_ssim`` — pytorch_msssim.ms_ssim (third-party, unvendored; called at
      attack_rd.py:336,362, self_ensemble.py:225,228).  SURVEY Appendix A.5(i):
      separable 11-tap Gaussian (sigma 1.5), VALID conv, per-(N,C) means, ReLU on
-     cs / ssim, avg_pool2d(2, padding=s%2).  Parity unpinned (no reference fixture).
+     cs / ssim, avg_pool2d(2, padding=s%2).  Pinned against the reference's own
+     independent NumPy MS-SSIM (utils/metrics_compare/msssim.py:119-178) through
+     tests/golden/msssim_np.npz (tests/test_msssim_np_golden.py).
 (ii) ``torch_msssim`` — utils/torch_msssim.py:26-71 (in-tree; used by
      adv_train.py:92,170).  2-D window min(H,W,11), sigma=1.5*ws/11, zero "same"
      padding, global mean per level, no ReLU, avg_pool2d(2,2).  Pinned by
