@@ -335,11 +335,9 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
 #pragma unroll
       for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
   };
-  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int u) {
-    ldw(nxt, u + 1);
-    // the next step's fragments are issued here, a whole step (48 MFMAs) ahead of their use: without the barrier
-    // the scheduler sank them next to their first use and waited on L2 latency every few MFMAs
-    __builtin_amdgcn_sched_barrier(0);
+  // the B operands (three LDS planes per pixel tile) of step u
+  auto ldb = [&](bf16x8 (&b)[PT][3], int u) {
+    u = min(u, total - 1);
     const int ti = u / NCG, c = u - ti * NCG;
     const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
     const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
@@ -347,21 +345,33 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
       const int o = e + t * 2 * XU_PC;   // tile t: 2 input rows down
-      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[(CG / 8) * XU_PLANE + o]),
-                           f4_as_bf8(patch[2 * (CG / 8) * XU_PLANE + o])};
-#pragma unroll
-      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], b, acc[t][it]);
+      b[t][0] = f4_as_bf8(patch[o]);
+      b[t][1] = f4_as_bf8(patch[(CG / 8) * XU_PLANE + o]);
+      b[t][2] = f4_as_bf8(patch[2 * (CG / 8) * XU_PLANE + o]);
     }
   };
-  bf16x8 fa[IT][3], fb[IT][3];
+  // one step: the next step's weight fragments AND LDS operands are issued first, a whole step (48 MFMAs) ahead of
+  // their use (without the barrier the scheduler sank the fragment loads next to their first use and waited on L2
+  // latency every few MFMAs; the LDS reads issued at the step's start exposed their latency to its first MFMA)
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], bf16x8 (&bc)[PT][3], bf16x8 (&bn)[PT][3], int u) {
+    ldw(nxt, u + 1);
+    ldb(bn, u + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], bc[t], acc[t][it]);
+  };
+  bf16x8 fa[IT][3], fb[IT][3], ba[PT][3], bb[PT][3];
   ldw(fa, 0);
+  ldb(ba, 0);
   int u = 0;
 #pragma unroll 1
   for (; u + 1 < total; u += 2) {
-    step(fa, fb, u);
-    step(fb, fa, u + 1);
+    step(fa, fb, ba, bb, u);
+    step(fb, fa, bb, ba, u + 1);
   }
-  if (u < total) step(fa, fb, u);
+  if (u < total) step(fa, fb, ba, bb, u);
 }
 
 template <int IT, int EPI, int CG>
