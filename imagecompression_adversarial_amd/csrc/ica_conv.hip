@@ -104,7 +104,9 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
   __shared__ f32x4 patch[NE * PLANE];
   // bf16 16-channel-chunk layers: the epilogue parameters in LDS (epi_params_to_lds), copied before the first
   // chunk fill, whose barriers publish them
-  constexpr bool LG = BF && CC == 16 && FX == 0;
+  // The RGB-input GDN forward too (g_a.0: 1.65 -> 1.31 ms at the config-5 shapes, although its 46 KB of LDS take it
+  // from 4 to 3 blocks per CU); the RGB GDN backward measured neutral and keeps the global loads.
+  constexpr bool LG = BF && FX == 0 && (CC == 16 || (CC == 4 && (EPI == EPI_GDN || EPI == EPI_IGDN)));
   __shared__ f32x4 lpar[LG ? epi_lds_entries<IT, EPI>() : 1];
 
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
