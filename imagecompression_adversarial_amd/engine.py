@@ -25,13 +25,6 @@ def _P(sd, prefix, name):
     return sd[f"{prefix}.{name}" if prefix else name]
 
 
-def _lowres(x4, down: int) -> int:
-    """Pixels per image of the low-resolution side of a k5 s2 layer fed x4 (nChw4c): its output for a conv_down
-    (down = 1), its input for a conv_up."""
-    H, W = x4.shape[2], x4.shape[3]
-    return ((H + 1) // 2) * ((W + 1) // 2) if down else H * W
-
-
 class Analysis:
     """g_a = conv(3,N)-GDN-conv(N,N)-GDN-conv(N,N)-GDN-conv(N,M), all k5 s2."""
 
@@ -50,22 +43,21 @@ class Analysis:
         h, C, saved = x4, 3, []
         for i in range(3):
             p = self.convs[i]
-            wp, pr = p.sel_fwd(_lowres(h, 1))
-            h, sx, ss = K.conv_down(h, C, wp, p.bias, self.N, 5, 2, K.EPI_GDN, self.gdns[i], save,
-                                    tag=f"{self.tag}.{2 * i}.fwd", prec=pr, it=p.it_fwd)
+            h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.gdns[i], save,
+                                    tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd)
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
-        wp, pr = p.sel_fwd(_lowres(h, 1))
-        y, _, _ = K.conv_down(h, self.N, wp, p.bias, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.6.fwd", prec=pr)
+        y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.6.fwd",
+                              prec=p.fwd_prec)
         return y, saved
 
     def backward(self, gy4, saved):
         g, C = gy4, self.M
         for i in (3, 2, 1):
-            wp, pr = self.convs[i].sel_bwd(_lowres(g, 0))
-            g, _, _ = K.conv_up(g, C, wp, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
-                                saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=pr, it=self.convs[i].it_bwd)
+            g, _, _ = K.conv_up(g, C, self.convs[i].bwd, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
+                                saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
+                                it=self.convs[i].it_bwd)
             C = self.N
         gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad",
                              prec=self.convs[0].bwd_prec)
@@ -90,9 +82,8 @@ class Synthesis:
         h, C, saved = y4, self.M, []
         for i in range(3):
             p = self.convs[i]
-            wp, pr = p.sel_fwd(_lowres(h, 0))
-            h, sx, ss = K.conv_up(h, C, wp, p.bias, self.N, K.EPI_IGDN, self.gdns[i], save,
-                                  tag=f"{self.tag}.{2 * i}.fwd", prec=pr, it=p.it_fwd)
+            h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gdns[i], save,
+                                  tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd)
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
@@ -102,12 +93,12 @@ class Synthesis:
     def backward(self, gx4, saved):
         g, C = gx4, 3
         for i in (3, 2, 1):
-            wp, pr = self.convs[i].sel_bwd(_lowres(g, 1))
-            g, _, _ = K.conv_down(g, C, wp, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gdns[i - 1],
-                                  saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=pr, it=self.convs[i].it_bwd)
+            g, _, _ = K.conv_down(g, C, self.convs[i].bwd, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gdns[i - 1],
+                                  saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
+                                  it=self.convs[i].it_bwd)
             C = self.N
-        wp, pr = self.convs[0].sel_bwd(_lowres(g, 1))
-        gy, _, _ = K.conv_down(g, self.N, wp, None, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad", prec=pr)
+        gy, _, _ = K.conv_down(g, self.N, self.convs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS,
+                               tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec)
         return gy
 
 

@@ -310,18 +310,6 @@ class PackedConv:
                 self.bwd_prec = PREC_X6
 
 
-    # The pack a launch uses (one place to choose; lowres_px = pixels per image of the layer's low-resolution side).
-    # x6 layers of any size stay on x6 operands: the library dispatches small grids (<= 32 x 32 per image) to its
-    # small-grid x6 kernels and 33x33..64x64 conv_down outputs to 128-pixel blocks.
-    def sel_fwd(self, lowres_px: int):
-        """(pack, prec) of the forward launch."""
-        return self.fwd, self.fwd_prec
-
-    def sel_bwd(self, lowres_px: int):
-        """(pack, prec) of the input-gradient launch."""
-        return self.bwd, self.bwd_prec
-
-
 class PackedGDN:
     def __init__(self, beta: torch.Tensor, gamma: torch.Tensor):
         C = beta.shape[0]
