@@ -306,15 +306,21 @@ __global__ __launch_bounds__(256, rgb_x6_wide<EPI>() ? 1 : 2) void conv_rgb_x6_k
 // conv_up_x6: weights [plane][cb][tap][chunk][it][lane] bf16x8.  Output y = 2a + PY uses taps ky = ky0 + 2i,
 // ky0 = (PY + 2) & 1, at input row a + (PY + 2 - ky) / 2 (conv_up_kernel's decomposition).
 // --------------------------------------------------------------------------------------------------------------
-constexpr int XU_TW = 16, XU_TH = 4 * X6_PT, XU_PC = XU_TW + 2, XU_PLANE = (XU_TH + 2) * XU_PC;  // 180 px
+// Block tile: 4 PT input rows x 16 columns; PT = 1 (64-pixel blocks) where the PT = 2 grid would end in a
+// partly-filled round of the 256 CUs (launch_up_x6): the same MFMA and epilogue sequence per output, so the same bits
+constexpr int XU_TW = 16, XU_PC = XU_TW + 2;
+template <int PT>
+constexpr int xu_th() { return 4 * PT; }
+template <int PT>
+constexpr int xu_plane() { return (xu_th<PT>() + 2) * XU_PC; }   // 180 px (PT = 2)
 
-template <int CG>
-constexpr int xu_lds_bytes() { return 3 * (CG / 8) * XU_PLANE * 16; }
+template <int CG, int PT>
+constexpr int xu_lds_bytes() { return 3 * (CG / 8) * xu_plane<PT>() * 16; }
 
-template <int PY, int PX, int IT, int CG>
+template <int PY, int PX, int IT, int CG, int PT>
 ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch, int grp, long ps,
-                              f32x16 (&acc)[X6_PT][IT]) {
-  constexpr int KS = 5, PAD = 2, PT = X6_PT;
+                              f32x16 (&acc)[PT][IT]) {
+  constexpr int KS = 5, PAD = 2, XU_PLANE = xu_plane<PT>();
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
   constexpr int NCG = CG / 16;   // 16-channel chunks per LDS group
@@ -374,9 +380,9 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
   if (u < total) step(fa, fb, ba, bb, u);
 }
 
-template <int IT, int EPI, int CG>
+template <int IT, int EPI, int CG, int PT = X6_PT>
 __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long ps) {
-  constexpr int PT = X6_PT, NQ = CG / 4;
+  constexpr int NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
   extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
   const int tiles_x = (p.Win + XU_TW - 1) / XU_TW, tiles_y = (p.Hin + XU_TH - 1) / XU_TH;
   int bid, cb;
@@ -438,7 +444,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
       for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
     for (int grp = 0; grp < ngrp; ++grp) {
       if (refill) fill(grp);
-      conv_up_x6_class<PY, PX, IT, CG>(p, patch, jt, cb, nch, grp, ps, acc);
+      conv_up_x6_class<PY, PX, IT, CG, PT>(p, patch, jt, cb, nch, grp, ps, acc);
     }
     X6T(tk);
     if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
@@ -812,22 +818,39 @@ int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
-template <int IT, int EPI, int CG>
-int launch_up_x6(const ConvParams& p, hipStream_t st) {
-  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + XU_TH - 1) / XU_TH) * p.N;
+template <int IT, int EPI, int CG, int PT>
+int launch_up_x6_pt(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<PT>() - 1) / xu_th<PT>()) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * 25 * (p.Cin / 16) * IT * 64;
-  constexpr size_t lds = xu_lds_bytes<CG>();
+  constexpr size_t lds = xu_lds_bytes<CG, PT>();
   static_assert(lds <= 160 * 1024, "conv_up_x6 channel group exceeds LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6_kernel<IT, EPI, CG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6_kernel<IT, EPI, CG, PT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_x6_kernel<IT, EPI, CG>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
+  hipLaunchKernelGGL((conv_up_x6_kernel<IT, EPI, CG, PT>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
+}
+
+// fraction of the launch's last round of 256 one-per-CU blocks that is busy, over all rounds
+static inline double x6_round_fill(long blocks) {
+  const long rounds = (blocks + 255) / 256;
+  return rounds ? (double)blocks / (double)(rounds * 256) : 1.0;
+}
+
+// PT = 1 when the PT = 2 grid leaves a partly-empty last round and halving the blocks fills the rounds clearly
+// better (config 2's 32x48-input layers: 384 blocks = 1.5 rounds -> 768 = 3 rounds); same bits either way
+template <int IT, int EPI, int CG>
+int launch_up_x6(const ConvParams& p, hipStream_t st) {
+  const long ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long b2 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N * ncb;
+  const long b1 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<1>() - 1) / xu_th<1>()) * p.N * ncb;
+  if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) return launch_up_x6_pt<IT, EPI, CG, 1>(p, st);
+  return launch_up_x6_pt<IT, EPI, CG, X6_PT>(p, st);
 }
 
 template <int IT, int EPI>

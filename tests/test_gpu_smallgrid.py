@@ -97,6 +97,26 @@ def test_x6_down_pt1_same_bits(K, B, hw):
     assert torch.equal(g1, g8[:1])
 
 
+def test_x6_up_pt1_same_bits(K):
+    """conv_up_x6 switches to PT = 1 (64-pixel blocks) when that fills the rounds of 256 CUs clearly better (32 images
+    of 32x48: 384 -> 768 blocks) and keeps PT = 2 for one image: the batch and its first image alone give the same
+    bits, for the IGDN forward (save) and the GDN-backward epilogues."""
+    B, h, w = 32, 32, 48
+    beta, gamma = _gdn(61)
+    gd = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
+    x = rnd((B, C, h, w), 62).to(DEV)
+    wt = rnd((C, C, 5, 5), 63) * 0.02
+    b = rnd((C,), 64) * 0.1
+    pd = K.PackedConv(wt.to(DEV), b.to(DEV), "deconv", 2, K.PREC_X6)
+    yB, _, sB = K.conv_up(K.to_nc4(x), C, pd.fwd, pd.bias, C, K.EPI_IGDN, gd, save=True, prec=pd.fwd_prec)
+    y1, _, s1 = K.conv_up(K.to_nc4(x[:1]), C, pd.fwd, pd.bias, C, K.EPI_IGDN, gd, save=True, prec=pd.fwd_prec)
+    assert torch.equal(y1, yB[:1]) and torch.equal(s1, sB[:1])
+    pc = K.PackedConv(wt.to(DEV), None, "conv", 2, K.PREC_X6)
+    gB, _, _ = K.conv_up(K.to_nc4(x), C, pc.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(yB, sB), prec=pc.bwd_prec)
+    g1, _, _ = K.conv_up(K.to_nc4(x[:1]), C, pc.bwd, None, C, K.EPI_GDN_BWD, gd, saved=(y1, s1), prec=pc.bwd_prec)
+    assert torch.equal(g1, gB[:1])
+
+
 # (h, w) of the synthesis layer's input: conv_up in h x w (small kernel iff h w <= 4096); the next deconv's
 # input-gradient conv_down writes 2h x 2w (split kernel iff 4 h w <= 4096)
 @pytest.mark.parametrize("prec", ["fp32", "x6"])
