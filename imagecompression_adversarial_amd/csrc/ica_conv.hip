@@ -25,22 +25,10 @@
 
 #include "ica_conv_epi.h"
 
+#include "ica_trace.h"
 #ifdef ICA_BF_TRACE
-// phase timestamps (s_memtime cycles) per (block, wave): experiment builds only (scripts/exp/bf_trace.py)
-__device__ unsigned long long ica_bf_trace[32768 * 4 * 8];
-#define BFT(k)                                                                                                 \
-  do {                                                                                                         \
-    if ((threadIdx.x & 63) == 0) {                                                                             \
-      const unsigned b_ = blockIdx.x + gridDim.x * blockIdx.y;                                                 \
-      if (b_ < 32768) ica_bf_trace[((size_t)b_ * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_readcyclecounter(); \
-    }                                                                                                          \
-  } while (0)
-extern "C" int ica_bf_trace_read(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ica_bf_trace), bytes, 0, hipMemcpyDeviceToHost);
-}
-extern "C" int ica_bf_trace_clear(const void* zeros, size_t bytes) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ica_bf_trace), zeros, bytes, 0, hipMemcpyHostToDevice);
-}
+ICA_TRACE_DEFINE(ica_bf_trace, ica_bf_trace_read, ica_bf_trace_clear)
+#define BFT(k) ICA_TRACE_STAMP(ica_bf_trace, k)
 #else
 #define BFT(k) \
   do {         \

@@ -26,22 +26,10 @@
 
 #include "ica_conv_epi.h"
 
+#include "ica_trace.h"
 #ifdef ICA_X6_TRACE
-// phase timestamps (s_memtime cycles) per (block, wave): experiment builds only (scripts/exp/x6_trace.py)
-__device__ unsigned long long ica_x6_trace[32768 * 4 * 8];
-#define X6T(k)                                                                                                 \
-  do {                                                                                                         \
-    if ((threadIdx.x & 63) == 0) {                                                                             \
-      const unsigned b_ = blockIdx.x + gridDim.x * blockIdx.y;                                                 \
-      if (b_ < 32768) ica_x6_trace[((size_t)b_ * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_readcyclecounter(); \
-    }                                                                                                          \
-  } while (0)
-extern "C" int ica_x6_trace_read(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(ica_x6_trace), bytes, 0, hipMemcpyDeviceToHost);
-}
-extern "C" int ica_x6_trace_clear(const void* zeros, size_t bytes) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(ica_x6_trace), zeros, bytes, 0, hipMemcpyHostToDevice);
-}
+ICA_TRACE_DEFINE(ica_x6_trace, ica_x6_trace_read, ica_x6_trace_clear)
+#define X6T(k) ICA_TRACE_STAMP(ica_x6_trace, k)
 #else
 #define X6T(k) \
   do {         \
