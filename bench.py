@@ -305,8 +305,8 @@ def main():
             args.batch = 8
         if args.precision is None:
             args.precision = "bf16"
-    if args.precision is None:   # the attack engine's default: x6 (fp32-accurate) for bmshj2018, fp32 for cheng2020
-        args.precision = "x6" if args.model == "hyper" else "fp32"
+    if args.precision is None:   # the attack engine's default: x6 (fp32-accurate)
+        args.precision = "x6"
     if args.precision == "bf16" and args.model != "hyper":
         raise SystemExit("the bf16 conv path covers the bmshj2018 transforms (config 5)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -341,7 +341,8 @@ def main():
     torch.manual_seed(0)
     net = models.cheng2020_anchor(args.quality) if model == "cheng2020" else models.bmshj2018_hyperprior(args.quality)
     sd = {k: v.detach().to(dev) for k, v in net.state_dict().items()}
-    kern = ChengKernels(sd) if model == "cheng2020" else CodecKernels(sd, "hyper", precision=args.precision)
+    kern = (ChengKernels(sd, precision=args.precision) if model == "cheng2020"
+            else CodecKernels(sd, "hyper", precision=args.precision))
     N, M = kern.N, kern.M
     gen = torch.Generator(device=dev).manual_seed(rank)
     im_s = torch.rand((B, 3, H, W), generator=gen, device=dev)
@@ -388,7 +389,7 @@ def main():
     dom_ms = per_tag[dom] if dom else 0.0
     dom_flops = tot_fl[dom] / len(hook[dom]) if dom else 0.0
     achieved = tot_fl[dom] / (tot_ms[dom] * 1e-3) / 1e12 if dom else 0.0
-    tag_prec = (dict(K.PREC_HOOK) or _tag_prec(kern)) if model == "hyper" else {}
+    tag_prec = (dict(K.PREC_HOOK) or _tag_prec(kern)) if model == "hyper" else dict(K.PREC_HOOK)
     peak = _peak(tag_prec.get(dom, 0))
     # HBM bytes per launch of the dominant kernel from the committed PMC passes of the same shapes
     # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)

@@ -649,11 +649,10 @@ class CompressionModel(nn.Module):
         return updated
 
     def attack_precision(self, requested: str | None = None) -> str:
-        """Conv operand precision of the attack engine: the request, else x6 (fp32-accurate bf16x6) for the
-        bmshj2018 / mbt2018 transforms and fp32 for cheng2020 (its k3 residual stacks have no x6 kernels)."""
-        if requested:
-            return requested
-        return "fp32" if self.model_kind == "cheng2020" else "x6"
+        """Conv operand precision of the attack engine: the request, else x6 (fp32-accurate bf16x6): the 5x5
+        stride-2 transforms of bmshj2018 / mbt2018, and cheng2020's 3x3 stride-1 residual convs (its strided,
+        subpel-gradient and RGB convs keep fp32 operands)."""
+        return requested or "x6"
 
     def kernels(self, precision: str = "fp32"):
         """Whole-model HIP executor (used by the attack engine).  precision 'bf16': bf16-operand g_a / g_s
@@ -662,9 +661,9 @@ class CompressionModel(nn.Module):
         if getattr(self, "_ck", None) is None or self._ck_key != key:
             sd = {k: v.detach() for k, v in self.state_dict().items()}
             if self.model_kind == "cheng2020":
-                if precision != "fp32":
+                if precision not in ("fp32", "x6"):
                     raise NotImplementedError("the bf16 conv path covers the bmshj2018 transforms")
-                self._ck = EC.ChengKernels(sd)
+                self._ck = EC.ChengKernels(sd, precision=precision)
             else:
                 self._ck = E.CodecKernels(sd, self.model_kind, precision=precision)
             self._ck_key = key

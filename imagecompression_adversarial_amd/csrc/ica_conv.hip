@@ -77,8 +77,11 @@ constexpr int conv_min_blocks() { return (KS == 5 && IT == 6) ? 1 : 2; }
 template <int KS, int IT, int CC, int EPI, bool BF>
 constexpr int conv_down_waves() { return (BF && CC == 4 && EPI == EPI_GDN) ? 4 : conv_min_blocks<KS, IT>(); }
 
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
-__global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
+// X6O: fp32-accurate bf16x6 operands (fp32 activations split into three bf16 planes as the patch is staged, the
+// three-plane weight pack of ica_pack_conv_weight_x6, six MFMAs per 16-deep k step; the epilogue is the fp32 one with
+// the fp32 gamma' pack): the k3 s1 layers of cheng2020 on the x6 ceiling.  One block per CU (512 registers).
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false>
+__global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
   constexpr int PT = down_pt<CC, BF>();
   constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
@@ -89,7 +92,8 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
   constexpr int NE = (BF && CC == 16) ? NQ / 2 : NQ;
   // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
-  __shared__ f32x4 patch[NE * PLANE];
+  static_assert(!X6O || (!BF && CC == 16 && (FX & FX_UNSHUF) == 0), "x6 conv_down: fp32 plain or masked fill");
+  __shared__ f32x4 patch[X6O ? 6 * PLANE : NE * PLANE];   // X6O: [plane][half][pixel], 8 channels as bf16
   // bf16 16-channel-chunk layers: the epilogue parameters in LDS (epi_params_to_lds), copied before the first
   // chunk fill, whose barriers publish them
   // The RGB-input GDN forward too (g_a.0: 1.65 -> 1.31 ms at the config-5 shapes, although its 46 KB of LDS take it
@@ -197,14 +201,20 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
       __syncthreads();
       return;
     }
-    if constexpr (!BF && CC == 16 && (FX & (FX_MASK | FX_UNSHUF)) == 0) {
+    if constexpr (!BF && CC == 16 && (FX & FX_UNSHUF) == 0 && (X6O || (FX & FX_MASK) == 0)) {
       // fp32 plain view (any epilogue extras): batches of FB 16-B buffer loads (32-bit offsets, out-of-image reads return zeros)
       // issued before their LDS writes, the first batch ahead of the barrier that ends the previous chunk's
-      // reads.  FB is kept small: these kernels run 3 waves/SIMD at <= 168 VGPRs.
+      // reads.  FB is kept small: these kernels run 3 waves/SIMD at <= 168 VGPRs.  X6O also takes the
+      // leaky-ReLU-masked view here (the mask quads load beside the activations; one block per CU, VGPRs spare).
+      constexpr bool MK = (FX & FX_MASK) != 0;
       constexpr int NF = (NE * PLANE + 255) / 256, FB = 3;
       const unsigned xplane = (unsigned)p.Hin * p.Win;
       const __amdgpu_buffer_rsrc_t xr =
           uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+      const __amdgpu_buffer_rsrc_t mr =
+          uniform_rsrc(reinterpret_cast<const char*>(MK ? p.mask : p.x) + (size_t)n * Cin4 * xplane * 16,
+                       MK ? Cin4 * xplane * 16u : 0u);
+      u32x4_t mv[MK ? FB : 1];
       auto batch = [&](int i0, u32x4_t (&v)[FB]) {
 #pragma unroll
         for (int i = 0; i < FB; ++i) {
@@ -216,13 +226,34 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
                           ix < p.Win;
           const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
           v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+          if constexpr (MK)
+            mv[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(mr, ok ? vo : 0xFFFFFFF0u, 0, 0));
         }
       };
       auto put = [&](int i0, const u32x4_t (&v)[FB]) {
 #pragma unroll
         for (int i = 0; i < FB; ++i) {
           const int e = threadIdx.x + 256 * (i0 + i);
-          if (i0 + i < NF && e < NE * PLANE) patch[e] = __builtin_bit_cast(f32x4, v[i]);
+          if (i0 + i < NF && e < NE * PLANE) {
+            if constexpr (X6O) {   // quad q of pixel pix -> three bf16 planes, half q >> 1, slot q & 1
+              const int q = e / PLANE, pix = e - q * PLANE;
+              f32x4 x = __builtin_bit_cast(f32x4, v[i]);
+              if constexpr (MK) {   // the generic fill's leaky-ReLU view, same fp32 ops
+                const f32x4 m = __builtin_bit_cast(f32x4, mv[i]);
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) x[e2] = m[e2] > 0.f ? x[e2] : x[e2] * 0.01f;
+              }
+              u32x2 a, b, c;
+              split3(x, a, b, c);
+              u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+              const int ent = (q >> 1) * PLANE + pix;
+              p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
+              p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+              p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+            } else {
+              patch[e] = __builtin_bit_cast(f32x4, v[i]);
+            }
+          }
         }
       };
       u32x4_t v[FB];
@@ -411,6 +442,38 @@ __global__ __launch_bounds__(256, (conv_down_waves<KS, IT, CC, EPI, BF>())) void
       step(fb, fa, g + 1);
     }
     if (g < NS) step(fa, fb, g);
+  } else if constexpr (X6O) {
+    // x6 operands: three bf16 weight-fragment planes (plane stride ps fragments), one step ahead (ping-pong)
+    const long ps = (long)((p.Cout + IT * 32 - 1) / (IT * 32)) * nch * KK * IT * 64;
+    const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+    const int wbase = cb * nch * KK * IT * 64;
+    auto ldw = [&](bf16x8 (&a)[IT][3], int g) {
+      const int f = wbase + min(g, total - 1) * IT * 64;
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+    };
+    auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) {
+      const int ch = g / KK, tap = g - ch * KK;
+      if (tap == 0) fill(ch);
+      ldw(nxt, g + 1);
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch a step ahead of its use
+      const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+      const int o = h * PLANE + lbase + ky * PC + kx;
+      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(cur[it], b, acc[0][it]);
+    };
+    bf16x8 fa[IT][3], fb[IT][3];
+    ldw(fa, 0);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 1 < total; g += 2) {
+      step(fa, fb, g);
+      step(fb, fa, g + 1);
+    }
+    if (g < total) step(fa, fb, g);
   } else {
     // Weight fragments stream linearly through (chunk, tap); they are prefetched
     // one tap ahead into the other of two register sets (ping-pong, no copies)
@@ -1340,14 +1403,58 @@ constexpr bool down_variant() {
 template <int KS, int S>
 constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) || (KS == 1 && S == 2); }
 
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false>
 static int launch_down(const ConvParams& p, hipStream_t st) {
   constexpr int TH = down_pt<CC, BF>() * 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
+}
+
+// x6 operands for the k3 s1 conv_downs (cheng2020 g_a / g_s and their input gradients): plain-view fills with the
+// residual / PixelShuffle extras; other extras (mask / unshuffle fills, t output) return -4 (the caller keeps fp32)
+template <int IT, int EPI, int FX>
+static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
+  if constexpr (!down_variant<3, 1, IT, EPI, FX>()) {
+    return -4;
+  } else {
+    if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true>(p, st);
+    return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true>(p, st);
+  }
+}
+template <int IT, int EPI>
+static int pick_fx_down_x6o(const ConvParams& p, int fx, hipStream_t st) {
+  switch (fx) {
+    case 0: return pick_tw_down_x6o<IT, EPI, 0>(p, st);
+    case FX_RES: return pick_tw_down_x6o<IT, EPI, FX_RES>(p, st);
+    case FX_PS: return pick_tw_down_x6o<IT, EPI, FX_PS>(p, st);
+    case FX_MASK: return pick_tw_down_x6o<IT, EPI, FX_MASK>(p, st);
+    default: return -4;
+  }
+}
+template <int IT>
+static int pick_epi_down_x6o(const ConvParams& p, int epi, int fx, hipStream_t st) {
+  switch (epi) {
+    case EPI_BIAS: return pick_fx_down_x6o<IT, EPI_BIAS>(p, fx, st);
+    case EPI_RELU: return pick_fx_down_x6o<IT, EPI_RELU>(p, fx, st);
+    case EPI_LRELU: return pick_fx_down_x6o<IT, EPI_LRELU>(p, fx, st);
+    case EPI_LRELU_BWD: return pick_fx_down_x6o<IT, EPI_LRELU_BWD>(p, fx, st);
+    case EPI_GDN: return pick_fx_down_x6o<IT, EPI_GDN>(p, fx, st);
+    case EPI_IGDN: return pick_fx_down_x6o<IT, EPI_IGDN>(p, fx, st);
+    case EPI_GDN_BWD: return pick_fx_down_x6o<IT, EPI_GDN_BWD>(p, fx, st);
+    case EPI_IGDN_BWD: return pick_fx_down_x6o<IT, EPI_IGDN_BWD>(p, fx, st);
+    default: return -5;
+  }
+}
+static int pick_down_x6o(const ConvParams& p, int it, int epi, int fx, hipStream_t st) {
+  if (p.Cin < 16) return -4;
+  switch (it) {
+    case 4: return pick_epi_down_x6o<4>(p, epi, fx, st);
+    case 6: return pick_epi_down_x6o<6>(p, epi, fx, st);
+    default: return -4;
+  }
 }
 
 // small-grid variant (conv_down_split_kernel): outputs of at most 64 x 64 pixels per image.  A per-image
@@ -1829,7 +1936,10 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   if (a->epi == EPI_LRELU_BWD && !a->in_x) return -4;
   const int fx = ((a->res || a->save_x) ? FX_RES : 0) | (a->ps ? FX_PS : 0) | (a->fill_mode == 1 ? FX_MASK : 0) |
                  (a->fill_mode == 2 ? FX_UNSHUF : 0) | (a->save_t ? FX_T : 0);
-  if (a->prec == 2) return ica_conv_x6_dispatch(p, a->kind, a->KS, a->S, it, a->epi, fx, st);
+  if (a->prec == 2) {
+    if (a->kind == 0 && a->KS == 3 && a->S == 1) return pick_down_x6o(p, it, a->epi, fx, st);
+    return ica_conv_x6_dispatch(p, a->kind, a->KS, a->S, it, a->epi, fx, st);
+  }
   if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, fx, st);
   if (a->kind == 1) return a->S == 2 ? pick_up(p, a->KS, it, a->epi, fx, st) : -6;
   return -6;

@@ -60,10 +60,13 @@ def _rho_weight(w, b, C):
     return wr.contiguous(), br.contiguous()
 
 
+X6_IT = (4, 6)   # row tiles of the x6 k3 s1 conv_down instantiations (ica_conv.hip pick_down_x6o)
+
+
 class Conv3:
     """One Conv2d(k in {1,3,5}, stride s, pad k//2) layer, packed for its forward and its input gradient."""
 
-    def __init__(self, w, b, stride=1, fwd_only=False, mask=None):
+    def __init__(self, w, b, stride=1, fwd_only=False, mask=None, x6=False):
         w = w.detach()
         if mask is not None:
             w = (w * mask.to(w.device)).contiguous()
@@ -83,31 +86,58 @@ class Conv3:
             else:             # dgrad = stride-2 transposed conv (conv_up, KS in {3, 1})
                 self.bwd = K.pack_conv(w, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, K.ORDER_UP, 16,
                                        it=self.it_b)
+        # x6 operands (fp32-accurate bf16x6) for the k3 s1 layers: three-plane packs of the same fragment orders
+        # (the input gradient's taps reversed by flipping the weight); launches with a PixelUnshuffle fill or
+        # that write t keep the fp32 packs
+        self.fwd6 = self.bwd6 = None
+        if x6 and stride == 1 and self.KS == 3 and self.Cin >= 16 and mask is None and self.it in X6_IT:
+            self.fwd6 = K.pack_conv_x6(w, self.Cout, self.Cin, 3, self.Cin * KK, KK, K.ORDER_DOWN, self.it)
+            if not fwd_only and self.Cout >= 16 and self.it_b in X6_IT:
+                self.bwd6 = K.pack_conv_x6(w.flip(-1, -2).contiguous(), self.Cin, self.Cout, 3, KK, self.Cin * KK,
+                                           K.ORDER_DOWN, self.it_b)
 
     def forward(self, x4, epi=K.EPI_BIAS, **kw):
+        if self.fwd6 is not None and _x6_ok(kw):
+            return K.conv_ex(x4, self.Cin, self.fwd6, self.bias, self.Cout, self.KS, self.S, 0, epi, self.it,
+                             prec=K.PREC_X6, **kw)
         return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.Cout, self.KS, self.S, 0, epi, self.it, **kw)
 
     def dgrad(self, g4, epi=K.EPI_BIAS, **kw):
         if self.S == 1:
+            if self.bwd6 is not None and _x6_ok(kw):
+                return K.conv_ex(g4, self.Cout, self.bwd6, None, self.Cin, self.KS, 1, 0, epi, self.it_b,
+                                 prec=K.PREC_X6, **kw)
             return K.conv_ex(g4, self.Cout, self.bwd, None, self.Cin, self.KS, 1, 0, epi, self.it_b, **kw)
         return K.conv_ex(g4, self.Cout, self.bwd, None, self.Cin, self.KS, 2, 1, epi, self.it_b, **kw)
+
+
+def _x6_ok(kw):
+    """An x6 k3 s1 launch: plain or leaky-ReLU-masked fill (no unshuffle) and no t output (ica_conv.hip
+    pick_down_x6o)."""
+    return kw.get("fill_mode", K.FILL_PLAIN) != K.FILL_UNSHUFFLE and kw.get("save_t") is None
 
 
 class Subpel:
     """subpel_conv3x3(Cin, C, 2) = Conv2d(Cin, 4C, 3, p=1) + PixelShuffle(2), rho-ordered rows."""
 
-    def __init__(self, w, b, fwd_only=False):
+    def __init__(self, w, b, fwd_only=False, x6=False):
         self.C = w.shape[0] // 4
         self.Cin = w.shape[1]
         wr, self.bias = _rho_weight(w, b, self.C)
         self.R = wr.shape[0]          # rho rows = 16 * ceil(C / 4)
         self.it = _it(self.R) if self.R != 768 else 6
         self.fwd = K.pack_conv(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, 16, it=self.it)
+        # x6 forward (PixelShuffle store, plain fill); the input gradient reads an unshuffled view: fp32
+        self.fwd6 = (K.pack_conv_x6(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, self.it)
+                     if x6 and self.Cin >= 16 and self.it in X6_IT else None)
         self.it_b = _it(self.Cin)
         self.bwd = None if fwd_only else K.pack_conv(wr, self.Cin, self.R, 3, 9, self.Cin * 9, K.ORDER_DOWN, 16,
                                                      flip=True, it=self.it_b)
 
     def forward(self, x4, epi=K.EPI_BIAS, **kw):
+        if self.fwd6 is not None and _x6_ok(kw):
+            return K.conv_ex(x4, self.Cin, self.fwd6, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,
+                             alg_rows=4 * self.C, prec=K.PREC_X6, **kw)
         return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,
                          alg_rows=4 * self.C, **kw)
 
@@ -124,7 +154,7 @@ def _gdn(sd, pre):
 class ChengAnalysis:
     """g_a = RBS(3,N) RB RBS RB RBS RB conv3x3 s2."""
 
-    def __init__(self, sd, prefix="g_a", tag="g_a"):
+    def __init__(self, sd, prefix="g_a", tag="g_a", x6=False):
         self.tag = tag
         self.N = sd[_k(prefix, "6.weight")].shape[0]
         self.M = self.N
@@ -133,12 +163,12 @@ class ChengAnalysis:
             pre = _k(prefix, str(i))
             if i % 2 == 0:
                 self.blocks.append(("rbs", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 2),
-                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1),
+                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6),
                                     Conv3(sd[f"{pre}.skip.weight"], sd[f"{pre}.skip.bias"], 2),
                                     _gdn(sd, f"{pre}.gdn")))
             else:
-                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1),
-                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1)))
+                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6),
+                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6)))
         self.last = Conv3(sd[_k(prefix, "6.weight")], sd[_k(prefix, "6.bias")], 2)
 
     def forward(self, x4, save=False):
@@ -191,7 +221,7 @@ class ChengAnalysis:
 class ChengSynthesis:
     """g_s = RB RBU RB RBU RB RBU RB subpel_conv3x3(N, 3, 2)."""
 
-    def __init__(self, sd, prefix="g_s", tag="g_s"):
+    def __init__(self, sd, prefix="g_s", tag="g_s", x6=False):
         self.tag = tag
         self.N = sd[_k(prefix, "0.conv1.weight")].shape[0]
         self.M = self.N
@@ -199,14 +229,15 @@ class ChengSynthesis:
         for i in range(7):
             pre = _k(prefix, str(i))
             if i % 2 == 0:
-                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1),
-                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1)))
+                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6),
+                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6)))
             else:
-                self.blocks.append(("rbu", Subpel(sd[f"{pre}.subpel_conv.0.weight"], sd[f"{pre}.subpel_conv.0.bias"]),
-                                    Conv3(sd[f"{pre}.conv.weight"], sd[f"{pre}.conv.bias"], 1),
-                                    Subpel(sd[f"{pre}.upsample.0.weight"], sd[f"{pre}.upsample.0.bias"]),
+                self.blocks.append(("rbu", Subpel(sd[f"{pre}.subpel_conv.0.weight"], sd[f"{pre}.subpel_conv.0.bias"],
+                                                  x6=x6),
+                                    Conv3(sd[f"{pre}.conv.weight"], sd[f"{pre}.conv.bias"], 1, x6=x6),
+                                    Subpel(sd[f"{pre}.upsample.0.weight"], sd[f"{pre}.upsample.0.bias"], x6=x6),
                                     _gdn(sd, f"{pre}.igdn")))
-        self.last = Subpel(sd[_k(prefix, "7.0.weight")], sd[_k(prefix, "7.0.bias")])
+        self.last = Subpel(sd[_k(prefix, "7.0.weight")], sd[_k(prefix, "7.0.bias")], x6=x6)
 
     def forward(self, y4, save=False):
         h, saved = y4, []
@@ -330,11 +361,16 @@ class ChengKernels:
 
     model = "cheng2020"
 
-    def __init__(self, sd: dict):
+    def __init__(self, sd: dict, precision: str = "fp32"):
+        """precision 'x6': the k3 s1 layers of g_a / g_s (the bulk of the work) on fp32-accurate bf16x6 operands;
+        strided, masked-fill and unshuffled-fill launches keep fp32 operands."""
         if sd["g_a.6.weight"].device.type != "cuda":
             raise RuntimeError("ChengKernels needs the state dict on the HIP device")
-        self.ga = ChengAnalysis(sd)
-        self.gs = ChengSynthesis(sd)
+        if precision not in ("fp32", "x6"):
+            raise NotImplementedError(f"cheng2020 operands: fp32 or x6, not {precision!r}")
+        x6 = precision == "x6"
+        self.ga = ChengAnalysis(sd, x6=x6)
+        self.gs = ChengSynthesis(sd, x6=x6)
         self.N = self.M = self.ga.N
         self.ha = ChengHA(sd)
         self.hs = ChengHS(sd)

@@ -460,15 +460,16 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
         if prec == PREC_BF16:
             gdn.bf16()
             gp = gdn.gpbT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpb
-        elif prec == PREC_X6:
+        elif prec == PREC_X6 and KS == 5:
             gdn.x6()
             gp = gdn.gpxT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpx
-        else:
+        else:   # fp32 epilogues (fp32 operands, and the x6 k3 s1 conv_downs: fp32 gamma' GEMMs)
             gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
     a = ConvArgs(ptr(x4), ptr(y), ptr(wp), ptr(bias), ptr(gp), ptr(None if gdn is None else gdn.beta), ptr(save_x),
                  ptr(save_s), ptr(in_x), ptr(in_s), ptr(save_t), ptr(res), ptr(mask), N, Cin, H, W, Cout, Ho, Wo,
                  kind, KS, S, epi, it, fill_mode, int(bool(ps)), int(prec))
     import ctypes
+    tag = _prec_note(tag, prec)
     ev = _ev_begin(tag, N)
     call("ica_conv_ex", ctypes.c_void_p(ctypes.addressof(a)), stream())
     if ev is not None:

@@ -1,0 +1,35 @@
+"""Trajectory-sensitivity sweep: cheng2020 q6 attack (2 x 64x64, 4 steps) on the fp32 and x6 HIP paths against the
+oracle over many input seeds; prints the noise deviation (max, fraction beyond 1e-3 of the noise max) per path.
+    python scripts/exp/cheng_seed_sweep.py [n_seeds]     # GPU box
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from oracle import attack as oa          # noqa: E402  (checker only)
+from oracle import codec as oc           # noqa: E402
+from imagecompression_adversarial_amd.attack import attack_batch              # noqa: E402
+from imagecompression_adversarial_amd.engine_cheng import ChengKernels        # noqa: E402
+
+DEV = torch.device("cuda:0")
+P = oc.perturb_params(oc.init_params("cheng2020", 6, seed=0), seed=1)
+kern = {pr: ChengKernels({k: v.to(DEV) for k, v in P.items()}, precision=pr) for pr in ("fp32", "x6")}
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+bad = {"fp32": 0, "x6": 0}
+for seed in range(100, 100 + n):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand((2, 3, 64, 64), generator=g)
+    rec = []
+    ref = oa.attack(P, x, steps=4, noise_thr=1e-5, model="cheng2020", eval_msssim=False, record=rec)
+    line = []
+    for pr, k in kern.items():
+        res = attack_batch(k, x.to(DEV), steps=4, noise_thr=1e-5, eval_msssim=False, record=True)
+        same = all([bool(v) for v in br] == [bool(v) for v in rec[i]["cheap"]] for i, br in enumerate(res.branches))
+        d = (res.noise.cpu() - ref.noise).abs() / ref.noise.abs().max()
+        out = float((d > 1e-3).float().mean())
+        bad[pr] += int(out > 0 or not same)
+        line.append(f"{pr} br {same} max {float(d.max()):.2e} >1e-3 {out:.4f}")
+    print(f"seed {seed}: " + " | ".join(line), flush=True)
+print("seeds with a deviation beyond 1e-3 or a branch change:", bad)
