@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
   constexpr int NE = (BF && CC == 16) ? NQ / 2 : NQ;
   // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
-  static_assert(!X6O || (!BF && CC == 16 && (FX & FX_UNSHUF) == 0), "x6 conv_down: fp32 plain or masked fill");
+  static_assert(!X6O || (!BF && CC == 16), "x6 conv_down: fp32 fills of 16-channel chunks");
   __shared__ f32x4 patch[X6O ? 6 * PLANE : NE * PLANE];   // X6O: [plane][half][pixel], 8 channels as bf16
   // bf16 16-channel-chunk layers: the epilogue parameters in LDS (epi_params_to_lds), copied before the first
   // chunk fill, whose barriers publish them
@@ -201,12 +201,13 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
       __syncthreads();
       return;
     }
-    if constexpr (!BF && CC == 16 && (FX & FX_UNSHUF) == 0 && (X6O || (FX & FX_MASK) == 0)) {
+    if constexpr (!BF && CC == 16 && (X6O || (FX & (FX_MASK | FX_UNSHUF)) == 0)) {
       // fp32 plain view (any epilogue extras): batches of FB 16-B buffer loads (32-bit offsets, out-of-image reads return zeros)
       // issued before their LDS writes, the first batch ahead of the barrier that ends the previous chunk's
       // reads.  FB is kept small: these kernels run 3 waves/SIMD at <= 168 VGPRs.  X6O also takes the
-      // leaky-ReLU-masked view here (the mask quads load beside the activations; one block per CU, VGPRs spare).
-      constexpr bool MK = (FX & FX_MASK) != 0;
+      // leaky-ReLU-masked view (the mask quads load beside the activations; one block per CU, VGPRs spare) and
+      // the PixelUnshuffle(2) view here (same image extent, only the quad offsets differ).
+      constexpr bool MK = (FX & FX_MASK) != 0, US = (FX & FX_UNSHUF) != 0;
       constexpr int NF = (NE * PLANE + 255) / 256, FB = 3;
       const unsigned xplane = (unsigned)p.Hin * p.Win;
       const __amdgpu_buffer_rsrc_t xr =
@@ -224,7 +225,13 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
           const int c4 = ch * NQ + q;
           const bool ok = i0 + i < NF && e < NE * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 &&
                           ix < p.Win;
-          const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+          unsigned vo;
+          if constexpr (US) {   // rho quad 4*c4g + sq of pixel (iy, ix): quad c4g of the 2x tensor at sub-pixel sq
+            const int c4g = c4 >> 2, sq = c4 & 3;
+            vo = (((unsigned)c4g * (2 * p.Hin) + 2 * iy + (sq >> 1)) * (2 * p.Win) + 2 * ix + (sq & 1)) * 16u;
+          } else {
+            vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+          }
           v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
           if constexpr (MK)
             mv[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(mr, ok ? vo : 0xFFFFFFF0u, 0, 0));
@@ -1431,6 +1438,8 @@ static int pick_fx_down_x6o(const ConvParams& p, int fx, hipStream_t st) {
     case FX_RES: return pick_tw_down_x6o<IT, EPI, FX_RES>(p, st);
     case FX_PS: return pick_tw_down_x6o<IT, EPI, FX_PS>(p, st);
     case FX_MASK: return pick_tw_down_x6o<IT, EPI, FX_MASK>(p, st);
+    case FX_UNSHUF: return pick_tw_down_x6o<IT, EPI, FX_UNSHUF>(p, st);
+    case FX_UNSHUF | FX_RES: return pick_tw_down_x6o<IT, EPI, FX_UNSHUF | FX_RES>(p, st);
     default: return -4;
   }
 }

@@ -87,8 +87,7 @@ class Conv3:
                 self.bwd = K.pack_conv(w, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, K.ORDER_UP, 16,
                                        it=self.it_b)
         # x6 operands (fp32-accurate bf16x6) for the k3 s1 layers: three-plane packs of the same fragment orders
-        # (the input gradient's taps reversed by flipping the weight); launches with a PixelUnshuffle fill or
-        # that write t keep the fp32 packs
+        # (the input gradient's taps reversed by flipping the weight); launches that write t keep the fp32 packs
         self.fwd6 = self.bwd6 = None
         if x6 and stride == 1 and self.KS == 3 and self.Cin >= 16 and mask is None and self.it in X6_IT:
             self.fwd6 = K.pack_conv_x6(w, self.Cout, self.Cin, 3, self.Cin * KK, KK, K.ORDER_DOWN, self.it)
@@ -112,9 +111,9 @@ class Conv3:
 
 
 def _x6_ok(kw):
-    """An x6 k3 s1 launch: plain or leaky-ReLU-masked fill (no unshuffle) and no t output (ica_conv.hip
+    """An x6 k3 s1 launch: any fill (plain, leaky-ReLU mask, PixelUnshuffle), no t output (ica_conv.hip
     pick_down_x6o)."""
-    return kw.get("fill_mode", K.FILL_PLAIN) != K.FILL_UNSHUFFLE and kw.get("save_t") is None
+    return kw.get("save_t") is None
 
 
 class Subpel:
@@ -127,12 +126,15 @@ class Subpel:
         self.R = wr.shape[0]          # rho rows = 16 * ceil(C / 4)
         self.it = _it(self.R) if self.R != 768 else 6
         self.fwd = K.pack_conv(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, 16, it=self.it)
-        # x6 forward (PixelShuffle store, plain fill); the input gradient reads an unshuffled view: fp32
+        # x6 forward (PixelShuffle store) and input gradient (PixelUnshuffle fill, the flipped weight)
         self.fwd6 = (K.pack_conv_x6(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, self.it)
                      if x6 and self.Cin >= 16 and self.it in X6_IT else None)
         self.it_b = _it(self.Cin)
         self.bwd = None if fwd_only else K.pack_conv(wr, self.Cin, self.R, 3, 9, self.Cin * 9, K.ORDER_DOWN, 16,
                                                      flip=True, it=self.it_b)
+        self.bwd6 = (K.pack_conv_x6(wr.flip(-1, -2).contiguous(), self.Cin, self.R, 3, 9, self.Cin * 9,
+                                    K.ORDER_DOWN, self.it_b)
+                     if x6 and not fwd_only and self.R >= 16 and self.it_b in X6_IT else None)
 
     def forward(self, x4, epi=K.EPI_BIAS, **kw):
         if self.fwd6 is not None and _x6_ok(kw):
@@ -143,6 +145,9 @@ class Subpel:
 
     def dgrad(self, g4, **kw):
         """g4: gradient of the shuffled output [N, C/4, 2H, 2W, 4] -> gradient of the input [N, Cin, H, W]."""
+        if self.bwd6 is not None and _x6_ok(kw):
+            return K.conv_ex(g4, self.R, self.bwd6, None, self.Cin, 3, 1, 0, K.EPI_BIAS, self.it_b,
+                             fill_mode=K.FILL_UNSHUFFLE, alg_rows=4 * self.C, prec=K.PREC_X6, **kw)
         return K.conv_ex(g4, self.R, self.bwd, None, self.Cin, 3, 1, 0, K.EPI_BIAS, self.it_b,
                          fill_mode=K.FILL_UNSHUFFLE, alg_rows=4 * self.C, **kw)
 
