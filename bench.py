@@ -401,6 +401,8 @@ def main():
         tfile = "pmc_traffic.json"
     elif args.precision == "bf16" and (H, W, B) == (2048, 2048, 8):
         tfile = "pmc_traffic_c5.json"
+    elif args.precision == "x6" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "cheng2020":
+        tfile = "pmc_traffic_c3x6.json"
     tf = os.path.join(REPO, "profiles", tfile) if tfile else None
     if tf and os.path.exists(tf):
         try:

@@ -7,7 +7,8 @@ Our loads/stores are 16 B per lane (nChw4c float4), so both corrections apply as
 
 Kernels are identified by (name prefix, Grid_Size); the grids follow the launchers in ica_conv.hip.
     python scripts/pmc_traffic.py gpurun_out/pmc [B H W prec] > profiles/pmc_traffic.json
-(default: 32 x 512x768 fp32; config 2 x6 = 32 512 768 x6; config 5 = 8 2048 2048 bf16).  Output {tag: bytes/launch}.
+(default: 32 x 512x768 fp32; config 2 x6 = 32 512 768 x6; config 5 = 8 2048 2048 bf16; config 3 = 32 512 768
+cheng_x6).  Output {tag: bytes/launch}.
 """
 import collections
 import csv
@@ -82,6 +83,15 @@ if PREC == "x6":   # ica_conv_x6.hip launchers (and the x6 Z-gather)
         "g_a.0.dgrad": up3_x6(*h[1]),
     }
 
+if PREC == "cheng_x6":   # cheng2020 q6 on x6 operands (config 3): the full-resolution k3 s1 launches with a
+    # (kernel, grid) of their own (conv_down_kernel X6O: 32 x 4 output pixels per block, IT = 6, Cout = 192)
+    def k3x6(epi, fx, Hout, Wout):
+        return (f"void conv_down_kernel<3, 1, 6, 16, 32, {epi}, {fx}, false, true>",
+                -(-Wout // 32) * -(-Hout // 4) * B * 256)
+
+    TAGS = {"g_s.6.conv1.dgrad": k3x6(5, 1, *h[1]), "g_a.1.conv1.dgrad": k3x6(4, 1, *h[1]),
+            "g_a.0.conv2.fwd": k3x6(2, 1, *h[1]), "g_s.5.conv.fwd": k3x6(3, 1, *h[1])}
+
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/p*/*_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
@@ -105,6 +115,7 @@ for tag, (prefix, grid) in TAGS.items():
     detail[tag] = {"read_bytes": rd, "write_bytes": wr}
 json.dump({**{k: round(v) for k, v in out.items()}, "_detail": detail,
            "_note": f"bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB*1024), gfx950 correction per "
-                    f"MI355X_MICROARCH.md HBM section; hyper q3, {B} x {H}x{W}, {PREC} conv operands"},
+                    f"MI355X_MICROARCH.md HBM section; {'cheng2020 q6' if PREC == 'cheng_x6' else 'hyper q3'}, "
+                    f"{B} x {H}x{W}, {PREC} conv operands"},
           sys.stdout, indent=1)
 print()
