@@ -78,8 +78,9 @@ def eval_forward(kern: CodecKernels, x: torch.Tensor, clamp=True):
     return out, K.bits_to_bpp(res["sumlog"], H * W)
 
 
-def padded_eval_forward(kern: CodecKernels, x: torch.Tensor, pad: int, mode="reflect", clamp=True):
-    """attack_rd.py:389-419 with -p: net(F.pad(x, (p, p, p, p), mode)) -> crop(x_hat), bits / (H * W)."""
+def padded_eval_forward(kern: CodecKernels, x: torch.Tensor, pad: int, mode="reflect"):
+    """attack_rd.py:389-419 with -p: net(F.pad(x, (p, p, p, p), mode)) -> crop(clamp(x_hat)), bits / (H * W).
+    The padded pre-eval clamps whatever --clamp says (attack_rd.py:417 clamps unconditionally)."""
     import torch.nn.functional as F
     B, _, H, W = x.shape
     xp = F.pad(x, (pad, pad, pad, pad), mode=mode).contiguous()
@@ -87,7 +88,7 @@ def padded_eval_forward(kern: CodecKernels, x: torch.Tensor, pad: int, mode="ref
     if Hp % 64 or Wp % 64:
         raise ValueError(f"-p {pad}: the padded size {Hp}x{Wp} must be a multiple of 64 (the codec's latent grid; "
                          "the reference's crop fails otherwise)")
-    out_p, bpp_p = eval_forward(kern, xp, clamp)
+    out_p, bpp_p = eval_forward(kern, xp, True)
     out = out_p[:, :, pad:pad + H, pad:pad + W].contiguous()
     return out, bpp_p * (Hp * Wp / (H * W))
 
@@ -173,7 +174,7 @@ class AttackLoop:
             # -p P (attack_rd.py:389-413): the pre-eval codes the image padded by P (-padmode, reflect by default),
             # output_s is the crop back to the image, bpp_ori counts the padded bits per UNPADDED pixel (:419);
             # the step loop and the post-eval run unpadded, as in the reference
-            self.output_s, self.bpp_ori = padded_eval_forward(kern, self.im_s, int(pad), padding_mode, clamp)
+            self.output_s, self.bpp_ori = padded_eval_forward(kern, self.im_s, int(pad), padding_mode)
         else:
             self.output_s, self.bpp_ori = eval_forward(kern, self.im_s, clamp)
         self.output_s4 = None

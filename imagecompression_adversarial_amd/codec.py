@@ -656,18 +656,25 @@ class CompressionModel(nn.Module):
 
     def kernels(self, precision: str = "fp32"):
         """Whole-model HIP executor (used by the attack engine).  precision 'bf16': bf16-operand g_a / g_s
-        convs (bmshj2018 models; BASELINE config 5)."""
-        key = (precision,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
-        if getattr(self, "_ck", None) is None or self._ck_key != key:
+        convs (bmshj2018 models; BASELINE config 5).  One executor per precision, each valid for one weight
+        version: the fine-tune's x6 inner attack and fp32 train step share a weight update without repacking
+        each other's executor (train.py adv_step -> RDTrainer.step)."""
+        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        cache = getattr(self, "_ck_cache", None)
+        if cache is None or cache[0] != key:
+            cache = (key, {})
+            self._ck_cache = cache
+        ex = cache[1].get(precision)
+        if ex is None:
             sd = {k: v.detach() for k, v in self.state_dict().items()}
             if self.model_kind == "cheng2020":
                 if precision not in ("fp32", "x6"):
                     raise NotImplementedError("the bf16 conv path covers the bmshj2018 transforms")
-                self._ck = EC.ChengKernels(sd, precision=precision)
+                ex = EC.ChengKernels(sd, precision=precision)
             else:
-                self._ck = E.CodecKernels(sd, self.model_kind, precision=precision)
-            self._ck_key = key
-        return self._ck
+                ex = E.CodecKernels(sd, self.model_kind, precision=precision)
+            cache[1][precision] = ex
+        return ex
 
 
 class FactorizedPrior(CompressionModel):

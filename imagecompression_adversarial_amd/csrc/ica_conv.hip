@@ -25,16 +25,6 @@
 
 #include "ica_conv_epi.h"
 
-#include "ica_trace.h"
-#ifdef ICA_BF_TRACE
-ICA_TRACE_DEFINE(ica_bf_trace, ica_bf_trace_read, ica_bf_trace_clear)
-#define BFT(k) ICA_TRACE_STAMP(ica_bf_trace, k)
-#else
-#define BFT(k) \
-  do {         \
-  } while (0)
-#endif
-
 // bf16 weight-fragment load of tile it at step g
 #define ICA_WLOAD_BF(w, it, g) ((w)[(it) * 64])
 
@@ -128,7 +118,6 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
   for (int t = 0; t < PT; ++t)
 #pragma unroll
     for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
-  BFT(0);
 
   // one 4-channel group of the conv input at (iy, ix), with the fill-mode view applied
   auto ldc4 = [&](int c4, int iy, int ix) -> f32x4 {
@@ -415,7 +404,6 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
     if (g < total) step(fr[0], fr[3], g);
     if (g + 1 < total) step(fr[1], fr[0], g + 1);
     if (g + 2 < total) step(fr[2], fr[1], g + 2);
-    BFT(2);
   } else if constexpr (CC == 4) {
     // fp32 RGB input, packed K (pack_conv_kernel, CC = 4): k-step m = 2g + s2 of step g takes the (tap,
     // channel) pair f = 2m + h from lane half h, f running over tap*Cin + channel.  With Cin = 3 that is
@@ -527,7 +515,6 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
     const int oy = oy0 + oyl[t], ox = ox0 + oxl[t];
     conv_epilogue<IT, EPI, FX, BF, 0, LG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lpar);
   }
-  BFT(3);
 }
 
 // --------------------------------------------------------------------------
@@ -815,9 +802,7 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
                            int nch, int tk) {
   f32x16 acc[up_pt<BF>()][IT];
   conv_up_acc<KS, PY, PX, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc);
-  BFT(tk);
   conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
-  BFT(tk + 1);
   (void)tk;
 }
 
@@ -865,7 +850,6 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   // The patch fill: batches of UP_FB entries per thread whose loads are all issued before their LDS writes
   // (buffer loads with 32-bit offsets into this image; padding pixels read past the descriptor and get
   // zeros), so the fill costs one memory latency per batch instead of one per entry.
-  BFT(0);
   const unsigned xplane = (unsigned)p.Hin * p.Win;
   const unsigned qbytes = BF ? 8u : 16u;
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(
@@ -897,7 +881,6 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
     }
   }
   __syncthreads();
-  BFT(1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int jt = wave & 1, nch = p.Cin / 16;
   // class pairs balance the tap counts: k5 9+4 | 6+6, k3 1+4 | 2+2
@@ -1420,8 +1403,9 @@ static int launch_down(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
-// x6 operands for the k3 s1 conv_downs (cheng2020 g_a / g_s and their input gradients): plain-view fills with the
-// residual / PixelShuffle extras; other extras (mask / unshuffle fills, t output) return -4 (the caller keeps fp32)
+// x6 operands for the k3 s1 conv_downs (cheng2020 g_a / g_s and their input gradients): plain, leaky-ReLU-mask and
+// PixelUnshuffle fills with the residual / PixelShuffle extras, IT 4 / 6; the t output (FX_T) and other extras
+// return -4 (nothing falls back here: engine_cheng._x6_ok keeps the fp32 pack for launches writing t)
 template <int IT, int EPI, int FX>
 static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
   if constexpr (!down_variant<3, 1, IT, EPI, FX>()) {

@@ -7,7 +7,7 @@
 //     a*b ~ ah*bh + ah*bm + am*bh + ah*bl + al*bh + am*bm
 // (dropped: am*bl + al*bm + al*bl, below 2^-24 relative, the size of one fp32 rounding).  bf16 x bf16 products are
 // exact in the fp32 accumulator, which adds them as the fp32 MFMA adds its own products, so the result has fp32
-// accuracy (scripts/exp/x6_down.cpp: max |err| vs float64 2.3e-6 where a sequential fp32 FMA chain gives 3.1e-6).
+// accuracy (measured in round 2: max |err| vs float64 2.3e-6 where a sequential fp32 FMA chain gives 3.1e-6).
 // Six v_mfma_f32_32x32x16_bf16 replace eight v_mfma_f32_32x32x2_f32 per 16-deep k step: 192 instead of 512 cycles.
 //
 // Storage stays fp32 (activations, saved tensors, gradients): the split happens when an input patch is staged into
@@ -26,21 +26,8 @@
 
 #include "ica_conv_epi.h"
 
-#include "ica_trace.h"
-#ifdef ICA_X6_TRACE
-ICA_TRACE_DEFINE(ica_x6_trace, ica_x6_trace_read, ica_x6_trace_clear)
-#define X6T(k) ICA_TRACE_STAMP(ica_x6_trace, k)
-#else
-#define X6T(k) \
-  do {         \
-  } while (0)
-#endif
-
 namespace {
 
-#ifndef X6_PF
-#define X6_PF 1   // conv_down_x6 patch prefetch: 0 none, 1 first batch during the previous chunk, 2 both batches
-#endif
 constexpr int X6_PT = 2;                 // 32-pixel tiles per wave
 constexpr int XD_TW = 32;
 // conv_down_x6 rows per block: 4 waves x PT tiles of one 32-pixel row each.  PT = 1 (128-pixel blocks, 71 KB of LDS)
@@ -138,17 +125,12 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
   // the next chunk's patch is loaded into registers during the last KK - TPF taps of the current one (both
   // batches, a straight-line tail so the waits stay exact) and staged into LDS between two barriers at the chunk
   // boundary: only the split and the LDS writes remain exposed (the fill's HBM latency was ~30 % of the loop)
-#ifndef X6_TPF
-#define X6_TPF 20
-#endif
-  constexpr int TPF = X6_TPF;
+  constexpr int TPF = 20;
   f32x4 v1[NB], v2[NB];
   auto chunk = [&](bf16x8 (&fa)[IT][3], bf16x8 (&fb)[IT][3], int ch) __attribute__((always_inline)) {
-    if constexpr (X6_PF < 0) batch(ch, 0, v1);
-    if constexpr (X6_PF == 1) batch(ch, NB, v2);
+    batch(ch, NB, v2);
     __syncthreads();
     put(0, v1);
-    if constexpr (X6_PF <= 0) batch(ch, NB, v2);
     put(NB, v2);
     __syncthreads();
     const int g0 = ch * KK, cn = min(ch + 1, nch - 1);
@@ -157,10 +139,7 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
       step(fa, fb, g0 + tp, tp, none);
       step(fb, fa, g0 + tp + 1, tp + 1, none);
     }
-    step(fa, fb, g0 + TPF, TPF, [&]() {
-      if constexpr (X6_PF >= 0) batch(cn, 0, v1);
-      if constexpr (X6_PF == 2) batch(cn, NB, v2);
-    });
+    step(fa, fb, g0 + TPF, TPF, [&]() { batch(cn, 0, v1); });
 #pragma unroll
     for (int tp = TPF + 1; tp < KK; ++tp) {
       if ((tp - TPF) & 1) step(fb, fa, g0 + tp, tp, none);
@@ -168,10 +147,8 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
     }
   };
   static_assert(TPF % 2 == 0 && KK % 2 == 1, "chunk parity: a chunk starting on fa ends with the next fragments in fb");
-  X6T(0);
   bf16x8 fa[IT][3], fb[IT][3];
-  if constexpr (X6_PF >= 0) batch(0, 0, v1);
-  if constexpr (X6_PF == 2) batch(0, NB, v2);
+  batch(0, 0, v1);
   ldw(fa, 0);
   int ch = 0;
 #pragma unroll 1
@@ -180,7 +157,6 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
     chunk(fb, fa, ch + 1);
   }
   if (ch < nch) chunk(fa, fb, ch);
-  X6T(2);
   if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
     const int oy[2] = {oy0 + wave * PT, oy0 + wave * PT + 1}, ox[2] = {ox0 + j, ox0 + j};
     gdn_fwd_x6_pair<IT, EPI>(p, acc, n, oy, ox);
@@ -191,7 +167,6 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
       conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
     }
   }
-  X6T(3);
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -202,13 +177,10 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
 // 9 steps of 16 (vs 25 x 4 channels): the kernel is epilogue- and store-heavy, so it runs 2 blocks per CU with one
 // 32-pixel tile per wave, the fill / epilogue of one block overlapping the MFMAs of the other.
 // --------------------------------------------------------------------------------------------------------------
-#ifndef X6_RGB_BWD_WIDE
-#define X6_RGB_BWD_WIDE 1
-#endif
 // GDN-backward epilogue: t, 2x and g*s for all 128 channels plus the u GEMM do not fit 256 registers (the narrow
 // form spilled or stashed g*s in the output); it runs 1 block per CU with the wide epilogue
 template <int EPI>
-constexpr int rgb_x6_wide() { return (EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD) && X6_RGB_BWD_WIDE; }
+constexpr int rgb_x6_wide() { return EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD; }
 
 template <int IT, int EPI>
 __global__ __launch_bounds__(256, rgb_x6_wide<EPI>() ? 1 : 2) void conv_rgb_x6_kernel(ConvParams p, long ps) {
@@ -224,7 +196,6 @@ __global__ __launch_bounds__(256, rgb_x6_wide<EPI>() ? 1 : 2) void conv_rgb_x6_k
   const int n = bid / tiles_y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
   const int oy0 = ty * TH, ox0 = tx * TW;
-  X6T(0);
   f32x16 acc[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
@@ -268,7 +239,6 @@ __global__ __launch_bounds__(256, rgb_x6_wide<EPI>() ? 1 : 2) void conv_rgb_x6_k
     }
   }
   __syncthreads();
-  X6T(1);
   auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) __attribute__((always_inline)) {
     if (g + 1 < KK) ldw(nxt, g + 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -283,11 +253,9 @@ __global__ __launch_bounds__(256, rgb_x6_wide<EPI>() ? 1 : 2) void conv_rgb_x6_k
     if (g & 1) step(fb, fa, g);
     else step(fa, fb, g);
   }
-  X6T(2);
   const int oy = oy0 + wave, ox = ox0 + j;
   conv_epilogue<IT, EPI, 0, false, rgb_x6_wide<EPI>() ? 1 : 2>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout,
                                                                cb * IT * 32);
-  X6T(3);
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -434,7 +402,6 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
       if (refill) fill(grp);
       conv_up_x6_class<PY, PX, IT, CG, PT>(p, patch, jt, cb, nch, grp, ps, acc);
     }
-    X6T(tk);
     if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
       const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
       const int ox[2] = {2 * (b0 + b_rel) + PX, 2 * (b0 + b_rel) + PX};
@@ -446,14 +413,11 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
         conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
       }
     }
-    X6T(tk + 1);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   const bool multi = ngrp > 1;
-  X6T(0);
   if (!multi) fill(0);
-  X6T(1);
   // every wave joins every fill barrier: both classes of every wave run the same group sequence
   if (wave < 2) {
     run_class(I0{}, I0{}, multi, 2);
@@ -874,7 +838,8 @@ int pick_up_x6(const ConvParams& p, hipStream_t st) {
 }  // namespace
 
 // x6 launches (ica_conv_ex with prec = 2): the k5 s2 conv (kind 0) and transposed conv (kind 1) layers of the
-// bmshj2018 transforms.  Returns -4 for shapes / epilogues without an x6 kernel (the caller keeps those fp32).
+// bmshj2018 transforms.  Returns -4 / -3 / -2 / -5 for shapes / epilogues without an x6 kernel: nothing falls back
+// here; hip_ops.x6_ok restates this coverage so that PackedConv keeps the fp32 pack for such layers.
 int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, int epi, int fx, hipStream_t st) {
   if (KS != 5 || S != 2 || fx != 0) return -4;
   if (p.Cout % 32 != 0) return -4;

@@ -172,10 +172,17 @@ def rgb_unshuffle_weight(w: torch.Tensor) -> torch.Tensor:
     return wp.view(O, 4, 3, 2, 3, 2).permute(0, 3, 5, 1, 2, 4).reshape(O, 16, 3, 3).contiguous()
 
 
-def x6_ok(O: int, C: int, it: int) -> bool:
-    """Layers the x6 kernels cover: k5 s2, >= 16 input channels, 128 output channels (IT 4, every epilogue) or
-    96-multiples at IT 3 (bias), no explicit 6-tile (C = 192 GDN) launch."""
-    return it == 0 and C >= 16 and C % 16 == 0 and (O % 128 == 0 or O % 96 == 0) and (C <= 128 or C % 64 == 0)
+def x6_ok(O: int, C: int, it: int, kind: int) -> bool:
+    """Shapes ica_conv_x6_dispatch (ica_conv_x6.hip) covers for a k5 s2 launch with O output / C input channels:
+    kind 0 (conv_down): C >= 16, a multiple of 16; O = 128-multiples (IT 4: bias, GDN, IGDN_BWD) or 96-multiples
+    (IT 3: bias only -- the only IT 3 conv_downs, g_a.6 forward and the g_s.0 input gradient, have no epilogue);
+    kind 1 (conv_up): IT 4 only (O a 128-multiple) with C = 64, 128 or a 64-multiple.  No explicit-IT (C = 192 GDN)
+    launch.  Anything else keeps the fp32 pack."""
+    if it != 0 or C < 16 or C % 16:
+        return False
+    if kind == 0:
+        return O % 128 == 0 or O % 96 == 0
+    return O % 128 == 0 and (C in (64, 128) or C % 64 == 0)
 
 
 def conv_cc(Cin: int) -> int:
@@ -292,20 +299,20 @@ class PackedConv:
             if self.Cin <= 4 and rgb_ok(self.Cout, self.it_fwd):   # forward from the RGB image: unshuffled k3 view
                 self.fwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cout, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
                 self.fwd_prec = PREC_X6
-            elif x6_ok(self.Cout, self.Cin, self.it_fwd):     # forward conv_down: o = co, c = ci
+            elif x6_ok(self.Cout, self.Cin, self.it_fwd, 0):  # forward conv_down: o = co, c = ci
                 self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN, x6_it(self.Cout))
                 self.fwd_prec = PREC_X6
-            if self.Cin != 3 and x6_ok(self.Cin, self.Cout, self.it_bwd):   # dgrad conv_up: o = ci, c = co
+            if self.Cin != 3 and x6_ok(self.Cin, self.Cout, self.it_bwd, 1):   # dgrad conv_up: o = ci, c = co
                 self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP, x6_it(self.Cin))
                 self.bwd_prec = PREC_X6
         else:
-            if self.Cout != 3 and x6_ok(self.Cout, self.Cin, self.it_fwd):  # forward conv_up: o = co, c = ci
+            if self.Cout != 3 and x6_ok(self.Cout, self.Cin, self.it_fwd, 1):  # forward conv_up: o = co, c = ci
                 self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP, x6_it(self.Cout))
                 self.fwd_prec = PREC_X6
             if self.Cout <= 4 and rgb_ok(self.Cin, self.it_bwd):   # dgrad from the RGB-sized gradient (view [ci][co])
                 self.bwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cin, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
                 self.bwd_prec = PREC_X6
-            elif x6_ok(self.Cin, self.Cout, self.it_bwd):       # dgrad conv_down: o = ci, c = co
+            elif x6_ok(self.Cin, self.Cout, self.it_bwd, 0):    # dgrad conv_down: o = ci, c = co
                 self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, x6_it(self.Cin))
                 self.bwd_prec = PREC_X6
 

@@ -1,6 +1,6 @@
 """Trajectory-sensitivity sweep: cheng2020 q6 attack (2 x 64x64, 4 steps) on the fp32 and x6 HIP paths against the
 oracle over many input seeds; prints the noise deviation (max, fraction beyond 1e-3 of the noise max) per path.
-    python scripts/exp/cheng_seed_sweep.py [n_seeds]     # GPU box
+    python scripts/cheng_seed_sweep.py [n_seeds]     # GPU box
 """
 import os
 import sys

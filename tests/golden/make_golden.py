@@ -267,8 +267,69 @@ def main_traj100():
     print("wrote", os.path.join(HERE, "traj100.npz"))
 
 
+# noise snapshots of the same trajectories (after these step indexes) and per-step noise fingerprints, so that a
+# run whose branch sequence leaves the reference's at step d can still be checked element-wise up to d
+SNAP_STEPS = (9, 24, 49)
+
+
+def fingerprint_pattern(shape):
+    return rand(shape, 977) * 2.0 - 1.0
+
+
+def main_traj100_snap():
+    """traj100.npz's runs again (same layers, weights, image and loop), recording noise after SNAP_STEPS and, per
+    step, (sum |noise|, sum noise^2, <noise, pattern>) with pattern a fixed seeded U(-1, 1) tensor."""
+    torch.set_num_threads(8)
+    rops, rtm, rau = _ref_modules()
+    out = {}
+    xs = traj100_image()
+    pat = fingerprint_pattern(xs.shape).double()
+    steps, eps_n, thr = 100, 16 / 255.0, 1e-4
+    B = lambda v, lo, hi: rops.Up_bound.apply(rops.Low_bound.apply(v, lo), hi)  # noqa: E731
+    ref = np.load(os.path.join(HERE, "traj100.npz"))
+    for tag in TRAJ100:
+        P = traj100_params(tag)
+        ga, gs = ref_stack(rops, rau, P, 128, 192)
+        with torch.no_grad():
+            os_ = torch.clamp(gs(torch.round(ga(xs))), 0, 1)
+        noise = torch.zeros_like(xs).requires_grad_(True)
+        opt = torch.optim.Adam([noise], lr=0.01)
+        sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1, 2, 3], gamma=0.33)
+        fp, snaps, branch = [], [], []
+        for i in range(steps):
+            nc = B(noise, -eps_n, eps_n)
+            im_in = B(xs + nc, 0.0, 1.0)
+            loss_i = torch.mean((xs - im_in) ** 2)
+            if loss_i > thr:
+                loss = loss_i
+                branch.append(1)
+            else:
+                o = B(gs(ga(im_in)), 0.0, 1.0)
+                loss = 1.0 - torch.mean((os_ - o) * (os_ - o))
+                branch.append(0)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            if i % (steps // 3) == 0:
+                sch.step()
+            n = noise.detach().double()
+            fp.append([float(n.abs().sum()), float((n * n).sum()), float((n * pat).sum())])
+            if i in SNAP_STEPS:
+                snaps.append(noise.detach().numpy().copy())
+        assert branch == [int(v) for v in ref[f"{tag}_branch"]], tag   # the same run as traj100.npz
+        assert np.array_equal(noise.detach().numpy(), ref[f"{tag}_noise"]), tag
+        out[f"{tag}_fp"] = np.array(fp, dtype=np.float64)
+        out[f"{tag}_snap"] = np.stack(snaps)
+        print(tag, "snapshots", SNAP_STEPS, flush=True)
+    out["snap_steps"] = np.array(SNAP_STEPS)
+    np.savez_compressed(os.path.join(HERE, "traj100_snap.npz"), **out)
+    print("wrote", os.path.join(HERE, "traj100_snap.npz"))
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "traj100":
         main_traj100()
+    elif len(sys.argv) > 1 and sys.argv[1] == "traj100_snap":
+        main_traj100_snap()
     else:
         main()

@@ -1,4 +1,5 @@
-"""One tiny attack step on cuda:0 checked against the CPU oracle (used by __graft_entry__.smoke)."""
+"""One tiny attack run on cuda:0, on the product default (x6 operands, the attack_rd / bench default), checked
+against the CPU oracle (used by __graft_entry__.smoke)."""
 import torch
 
 from oracle import codec
@@ -16,18 +17,18 @@ def run_smoke():
     from imagecompression_adversarial_amd import _lib
     dev = torch.device("cuda:0")
     P, Pd = _params(dev)
-    kern = CodecKernels(Pd, "hyper")
-    x = torch.rand((1, 3, 64, 64), generator=torch.Generator().manual_seed(7))
+    kern = CodecKernels(Pd, "hyper", precision="x6")
+    x = torch.rand((2, 3, 64, 128), generator=torch.Generator().manual_seed(7))
     res = attack_batch(kern, x.to(dev), steps=3, eval_msssim=False)
     ref = oatt.attack(P, x, steps=3, eval_msssim=False)
     torch.cuda.synchronize()
     err_s = (res.output_s.cpu() - ref.output_s).abs().max().item()
     err_n = (res.noise.cpu() - ref.noise).abs().max().item() / max(ref.noise.abs().max().item(), 1e-30)
-    err_b = abs(res.bpp_ori.item() - ref.bpp_ori.item())
+    err_b = (res.bpp_ori.cpu() - ref.bpp_ori).abs().max().item()
     assert err_s < 1e-4, f"output_s mismatch {err_s}"
     assert err_n < 1e-3, f"noise mismatch {err_n}"
     assert err_b < 1e-3, f"bpp mismatch {err_b}"
-    print(f"smoke ok: lib={_lib.LIB_PATH} |d output_s|={err_s:.2e} rel|d noise|={err_n:.2e} |d bpp|={err_b:.2e}")
+    print(f"smoke ok ({kern.precision}): lib={_lib.LIB_PATH} |d output_s|={err_s:.2e} rel|d noise|={err_n:.2e} |d bpp|={err_b:.2e}")
 
 
 if __name__ == "__main__":

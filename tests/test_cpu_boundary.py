@@ -27,6 +27,75 @@ def test_library_exports_header_symbols():
     assert set(_lib.exported_symbols()) <= set(syms)
 
 
+def header_prototypes():
+    """name -> list of argument classes ('p' pointer / stream, 'i' int, 'l' long, 'f' float, 'z' size_t) and the
+    return class, parsed from every `int|long|size_t ica_*(...)` prototype of include/ica_hip.h."""
+    txt = open(os.path.join(REPO, "include", "ica_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", " ", txt, flags=re.S)
+    out = {}
+    for ret, name, args in re.findall(r"^(int|long|size_t)\s+(ica_\w+)\s*\(([^)]*)\)\s*;", txt, re.M):
+        cls = []
+        a = " ".join(args.split())
+        if a not in ("", "void"):
+            for arg in a.split(","):
+                arg = arg.strip()
+                if "*" in arg or arg.startswith("hipStream_t"):
+                    cls.append("p")
+                else:
+                    typ = arg.rsplit(" ", 1)[0].replace("const ", "").strip()
+                    cls.append({"int": "i", "long": "l", "float": "f", "size_t": "z"}[typ])
+        out[name] = (cls, {"int": "i", "long": "l", "size_t": "z"}[ret])
+    return out
+
+
+def _ctype_class(t):
+    import ctypes as C
+    return {C.c_void_p: "p", C.c_int: "i", C.c_long: "l", C.c_float: "f", C.c_size_t: "z"}[t]
+
+
+def test_bindings_match_header_prototypes():
+    """Every ctypes binding in _lib._SIGS has the argument count, per-argument class (pointer / int / long /
+    float / size_t) and return class of its include/ica_hip.h prototype: a stale binding or header fails here."""
+    from imagecompression_adversarial_amd import _lib
+    protos = header_prototypes()
+    assert set(protos) == set(header_symbols())
+    for name, args in _lib._SIGS.items():
+        assert name in protos, name
+        want, ret = protos[name]
+        got = [_ctype_class(t) for t in args]
+        assert got == want, (name, "".join(got), "".join(want))
+        assert _ctype_class(_lib._RESTYPES.get(name, _lib._i)) == ret, name
+
+
+def test_integration_snippet_matches_header():
+    """The ctypes stub INTEGRATION.md shows a maintainer (`lib.<name>.argtypes = [...]`) declares each entry point
+    exactly as include/ica_hip.h does."""
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    protos = header_prototypes()
+    decl = re.findall(r"lib\.(ica_\w+)\.argtypes\s*=\s*\[([^\]]*)\]", doc)
+    assert len(decl) >= 2
+    letter = {"P": "p", "I": "i", "F": "f", "L": "l", "Z": "z"}
+    for name, lst in decl:
+        got = [letter[x.strip()] for x in lst.split(",") if x.strip()]
+        assert got == protos[name][0], (name, "".join(got), "".join(protos[name][0]))
+    # every call of a declared entry point in the snippet passes as many arguments as the prototype takes
+    ncalls = 0
+    for name, _ in decl:
+        for mt in re.finditer(r"lib\.%s\(" % name, doc):
+            depth, n, j = 1, 0, mt.end()
+            empty = doc[j] == ")"
+            while depth:
+                ch = doc[j]
+                depth += ch in "(["
+                depth -= ch in ")]"
+                n += ch == "," and depth == 1
+                j += 1
+            n = 0 if empty else n + 1
+            assert n == len(protos[name][0]), (name, n, len(protos[name][0]))
+            ncalls += 1
+    assert ncalls >= len(decl)
+
+
 def test_no_oracle_import_in_product():
     pkg = os.path.join(REPO, "imagecompression_adversarial_amd")
     for root, _, files in os.walk(pkg):

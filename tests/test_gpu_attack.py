@@ -328,5 +328,11 @@ def test_pad_pre_eval_vs_oracle(hyper3):
     assert rel_err(res.output_s.cpu(), ref.output_s) < 1e-4
     assert torch.allclose(res.bpp_ori.cpu(), ref.bpp_ori, rtol=1e-4, atol=1e-5)
     assert rel_err(res.noise.cpu(), ref.noise) < 2e-3
+    # --no-clamp -p: the padded pre-eval still clamps output_s (attack_rd.py:417), the step loop does not
+    res = attack_batch(kern, x.to(DEV), steps=3, pad=32, clamp=False, eval_msssim=False)
+    ref = oatt.attack(P, x, steps=3, pad=32, clamp=False, eval_msssim=False)
+    assert float(res.output_s.min()) >= 0.0 and float(res.output_s.max()) <= 1.0
+    assert rel_err(res.output_s.cpu(), ref.output_s) < 1e-4
+    assert rel_err(res.noise.cpu(), ref.noise) < 2e-3
     with pytest.raises(ValueError):
         attack_batch(kern, x.to(DEV), steps=1, pad=8)

@@ -258,7 +258,7 @@ def test_cheng_x6_attack_localized_divergence(cheng6x6):
     elements, in one region, leave the 1e-3 band (max 6.5e-2 of the noise max; the fp32 path stays at 6.8e-4).
     The transforms agree with the oracle at fp32 level on this input (y 1.7e-6, input gradient 2.1e-6 of max).
     This is the attack's own trajectory sensitivity, not an x6 defect: over 24 further seeds
-    (scripts/exp/cheng_seed_sweep.py, profiles/r02b/cheng_seed_sweep.log) the fp32 path shows such a localized
+    (scripts/cheng_seed_sweep.py, profiles/r02b/cheng_seed_sweep.log) the fp32 path shows such a localized
     divergence on 12 and x6 on 9, both with every branch matching.  Bounded here rather than hidden."""
     from imagecompression_adversarial_amd.attack import attack_batch
     P, kern = cheng6x6
