@@ -14,8 +14,8 @@ Checks and stated tolerances:
     per image (the batch-independence the speculative / compacted attack step relies on, attack.py _select);
   * branch compaction on x6 at B = 32 with mixed branches (sub-batches of 21 images): compacted == full-batch
     network step, bit for bit, over 3 steps;
-  * cheng2020 q6 (config 3), B = 1, 512x768, x6: g_a + g_s forward and input gradient vs the oracle at the
-    cheng tolerances (2e-4 / 2e-3).
+  * cheng2020 q6 (config 3), B = 1, 512x768, x6: g_a + g_s forward vs the oracle (2e-4); forward and input
+    gradient against float64, no worse than 2x the fp32 oracle's own error (+ 2e-6 of max).
 """
 import pytest
 import torch
@@ -113,6 +113,11 @@ def test_hyper_headline_compaction_bitexact(hyper3):
 
 
 def test_cheng_headline_chain_vs_oracle():
+    """cheng2020's g_a + g_s at 512x768, forward vs the fp32 oracle (2e-4), and -- for the input gradient, whose
+    13 leaky-ReLU residual blocks make it kink-sensitive at this size -- against a float64 evaluation of the same
+    chain: the x6 path must be at least as accurate as the fp32 oracle itself, within 2x its error plus an fp32
+    floor of 2e-6 of the tensor max.  (Measured: the fp32 oracle's input gradient is 2.6e-3 of max away from
+    float64 at one leaky-ReLU kink (216, 648), the fp32 HIP path likewise, x6 1.3e-3; scripts/accuracy_diag.py.)"""
     from imagecompression_adversarial_amd import hip_ops as K
     from imagecompression_adversarial_amd.engine_cheng import ChengKernels
     torch.set_num_threads(16)
@@ -121,12 +126,20 @@ def test_cheng_headline_chain_vs_oracle():
     x = rnd((1, 3, H, W), 48)
     y4, sa = kern.g_a(K.to_nc4(x.to(DEV)), save=True)
     xh4, ss = kern.g_s(y4, save=True)
-    xr = x.clone().requires_grad_(True)
-    yr = codec.cheng_g_a(P, xr)
-    xhr = codec.cheng_g_s(P, yr)
-    assert rel_err(K.from_nc4(y4, 192).cpu(), yr.detach()) < 2e-4
-    assert rel_err(K.from_nc4(xh4, 3).cpu(), xhr.detach()) < 2e-4
-    gout = rnd(xhr.shape, 49, -1, 1)
-    xhr.backward(gout)
+    got = [K.from_nc4(y4, 192).cpu(), K.from_nc4(xh4, 3).cpu()]
+    gout = rnd(got[1].shape, 49, -1, 1)
     gx4 = kern.g_a_backward(kern.g_s_backward(K.to_nc4(gout.to(DEV)), ss), sa)
-    assert rel_err(K.from_nc4(gx4, 3).cpu(), xr.grad) < 2e-3
+    got.append(K.from_nc4(gx4, 3).cpu())
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        Pd = {k: v.to(dt) for k, v in P.items()}
+        xr = x.to(dt).clone().requires_grad_(True)
+        yr = codec.cheng_g_a(Pd, xr)
+        xhr = codec.cheng_g_s(Pd, yr)
+        xhr.backward(gout.to(dt))
+        refs[dt] = (yr.detach(), xhr.detach(), xr.grad)
+    assert rel_err(got[0], refs[torch.float32][0]) < 2e-4
+    assert rel_err(got[1], refs[torch.float32][1]) < 2e-4
+    for name, g, r32, r64 in zip(("y", "x_hat", "input grad"), got, refs[torch.float32], refs[torch.float64]):
+        e6, e32 = rel_err(g, r64), rel_err(r32, r64)
+        assert e6 <= 2.0 * e32 + 2e-6, (name, e6, e32)
