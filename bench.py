@@ -286,6 +286,11 @@ def main():
                          "all-reduce), 5 targeted ROI hyper q3 2048x2048 bf16")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mixed", type=float, default=None, metavar="SCALE",
+                    help="also time one whole 1001-step run with g_a's last weight scaled by SCALE (40: O(1) latents "
+                         "as a trained codec has, so the run hovers at the -noise budget and both branches occur; "
+                         "make_golden.py TRAJ100) and report its branch census, rate and host branch-read cost "
+                         "next to the (unchanged, all-network-branch) headline")
     ap.add_argument("--full-run", dest="full_run", type=int, default=None,
                     help="1: also run the whole 1001-step loop once (wall time + branch census of the full run); "
                          "default 1 for the hyperprior configs at N = 1, 0 for cheng2020 (~7 min)")
@@ -431,6 +436,28 @@ def main():
                 "expensive_frac": round(fx / (B * 1001), 4)}
         del loop2
 
+    # mixed branches (N == 1, hyperprior): trained-scale latents, one whole 1001-step run
+    mixed = None
+    if world == 1 and args.mixed and model == "hyper":
+        sd2 = dict(sd)
+        sd2["g_a.6.weight"] = sd["g_a.6.weight"] * float(args.mixed)
+        kern2 = CodecKernels(sd2, "hyper", precision=args.precision)
+        loop3 = AttackLoop(kern2, im_s, steps=1001, **roi_kw)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(1001):
+            loop3.step(i)
+        torch.cuda.synchronize()
+        fe = time.perf_counter() - t1
+        fx = loop3.expensive_image_steps()
+        mixed = {"weight_scale": args.mixed, "steps": 1001, "wall_s": round(fe, 3),
+                 "value": round(B * 1001 / fe, 3), "expensive_image_steps": fx, "image_steps": B * 1001,
+                 "expensive_frac": round(fx / (B * 1001), 4),
+                 "steps_waiting_for_branch_read": loop3.sync_steps,
+                 "branch_read_wait_s": round(loop3.sync_wait_s, 3),
+                 "ms_per_step": round(fe / 1001 * 1e3, 3)}
+        del loop3, kern2
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -462,6 +489,7 @@ def main():
             "branch_census": {"expensive_image_steps": exp_steps, "image_steps": B * args.steps,
                               "expensive_frac": round(exp_steps / (B * args.steps), 4)},
             "full_run": full,
+            "mixed_branch_run": mixed,
             "step_gflop_per_image": round(total_flops / B / 1e9, 2),
             "step_tflops": round(total_flops / (ms_step * 1e-3) / 1e12, 2),
             "step_roofline_frac": round(total_flops / (ms_step * 1e-3) / 1e12 /

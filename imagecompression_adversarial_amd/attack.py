@@ -26,6 +26,7 @@ random start (the reference default path), per image.
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass, field
 
 import torch
@@ -169,6 +170,10 @@ class AttackLoop:
         self._sel_pending = False
         self.census = torch.zeros(B, dtype=torch.int32, device=dev)
         self.steps_done = 0
+        # host-side cost of the branch read: steps whose network launch waited for the device's selection, and the
+        # wall time spent blocked in those waits (bench.py --mixed reports them)
+        self.sync_steps = 0
+        self.sync_wait_s = 0.0
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
         if pad:
             # -p P (attack_rd.py:389-413): the pre-eval codes the image padded by P (-padmode, reflect by default),
@@ -212,7 +217,10 @@ class AttackLoop:
         if prev_all and (self.metric == "L2" or self.roi is not None):   # speculate: the whole batch, no wait
             self._sel_pending = True
             return B, None
+        t0 = time.perf_counter()
         self._sel_ev.synchronize()
+        self.sync_wait_s += time.perf_counter() - t0
+        self.sync_steps += 1
         E = int(self.sel_host[0])
         if E == B:
             self._sel_pending = True   # (already complete) lets the next step speculate

@@ -137,6 +137,19 @@ ICA_DEV float wave_sum(float v) {
   return v;
 }
 
+// Compute units of the current device (host side; persistent launches size their grid to it).
+inline int ica_cu_count() {
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = v;
+    else
+      cus = 256;
+  }
+  return cus;
+}
+
 #define ICA_CHECK_LAUNCH()                          \
   do {                                              \
     hipError_t _e = hipGetLastError();              \

@@ -1238,6 +1238,149 @@ gather:
   }
 }
 
+// --------------------------------------------------------------------------
+// conv_up3 on x6 operands, persistent and pipelined (the default for Cin = 128 / 192).  A tile is R = 4 CT - 2 input
+// rows x 30 columns; its Z = W^T x (75 x Cin, fp32-accurate bf16x6 MFMAs) covers the (R + 2) x 32 halo, i.e. exactly
+// one 32-pixel MFMA column tile per halo row, CT rows per wave (Z in LDS: 75 x 4 CT x 32 floats; the halo costs
+// (R + 2) x 32 / (R x 30) = 1.28x at CT = 3 instead of the 5 x 32 tile's 1.49x).  Each block walks a contiguous run of
+// tiles; the activations of tile t+1 are loaded into the registers of tile t's as each chunk is consumed (one whole
+// tile of prefetch distance, no extra registers), so the kernel streams instead of waiting out one HBM round trip per
+// chunk (the 5 x 32 kernel ran 8 dependent chunk loads per tile: latency-bound at 0.17 of the x6 ceiling).
+// Weights: the pack_up3_x6 fragments, one chunk's 9 fragments a chunk ahead, shared by the CT column tiles.
+// --------------------------------------------------------------------------
+constexpr int U3_OW = 30, U3_HW = 32;
+template <int CT>
+constexpr int u3_rows() { return 4 * CT - 2; }
+template <int CT>
+constexpr int u3_npx() { return 4 * CT * U3_HW; }
+
+template <int NCH, int CT>
+__global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int tiles_per_block) {
+  constexpr int R = u3_rows<CT>(), NPX = u3_npx<CT>();
+  __shared__ float zs[T3_ROWS * NPX];
+  const int tiles_x = (p.Win + U3_OW - 1) / U3_OW, tiles_y = (p.Hin + R - 1) / R;
+  const int total = tiles_x * tiles_y * p.N;
+  int blk, by;
+  xcd_block<true>(blk, by);
+  (void)by;
+  const int t_begin = blk * tiles_per_block, t_end = min(total, t_begin + tiles_per_block);
+  if (t_begin >= t_end) return;   // block-uniform
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Cin4 = p.Cin >> 2;
+  const unsigned plane = (unsigned)p.Hin * p.Win;
+  auto coords = [&](int t, int& n, int& a0, int& b0) {
+    const int tx = t % tiles_x, r = t / tiles_x;
+    a0 = (r % tiles_y) * R;
+    b0 = tx * U3_OW;
+    n = r / tiles_y;
+  };
+  // activations of (column tile ct, chunk ch): channels 16 ch + 8 h .. + 7 of halo pixel (row wave + 4 ct, col j);
+  // pixels outside the image read past the descriptor's range (zeros)
+  f32x4 xa[CT][NCH][2];
+  auto load_chunk = [&](int t, int ct, int ch) __attribute__((always_inline)) {
+    int n, a0, b0;
+    coords(t, n, a0, b0);
+    const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
+    const int iy = a0 - 1 + wave + 4 * ct, ix = b0 - 1 + j;
+    const bool ok = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+    const unsigned o0 = ok ? ((unsigned)(4 * ch + 2 * h) * plane + (unsigned)iy * p.Win + ix) * 16u : 0xFFFFFFF0u;
+    xa[ct][ch][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o0, 0, 0));
+    xa[ct][ch][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? o0 + plane * 16u : 0xFFFFFFF0u,
+                                                                                     0, 0));
+  };
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) load_chunk(t_begin, ct, ch);
+  constexpr long pst = 3L * NCH * 64;   // fragments per plane
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * pst * 16));
+  int wz = 0;   // a per-tile "zero" (keeps the fragment offsets from being hoisted into SGPRs across the tile loop)
+  auto ldw = [&](bf16x8 (&a)[3][3], int ch) {
+#pragma unroll
+    for (int it = 0; it < 3; ++it)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, wz + (int)((q * pst + ((long)it * NCH + ch) * 64) * 16));
+  };
+  const float bias0 = p.bias ? p.bias[0] : 0.f, bias1 = p.bias ? p.bias[1] : 0.f, bias2 = p.bias ? p.bias[2] : 0.f;
+#pragma unroll 1
+  for (int t = t_begin; t < t_end; ++t) {
+    wz = 0;
+    asm volatile("" : "+s"(wz));
+    const bool more = t + 1 < t_end;
+    f32x16 acc[CT][3];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int it = 0; it < 3; ++it) acc[ct][it] = f32x16{0};
+    bf16x8 wa[2][3][3];
+    ldw(wa[0], 0);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      if (ch + 1 < NCH) ldw(wa[(ch + 1) & 1], ch + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const float v[8] = {xa[ct][ch][0][0], xa[ct][ch][0][1], xa[ct][ch][0][2], xa[ct][ch][0][3],
+                            xa[ct][ch][1][0], xa[ct][ch][1][1], xa[ct][ch][1][2], xa[ct][ch][1][3]};
+        bf16x8 b[3];
+        split3x8(v, b);
+#pragma unroll
+        for (int it = 0; it < 3; ++it) acc[ct][it] = mfma_x6(wa[ch & 1][it], b, acc[ct][it]);
+        if (more) load_chunk(t + 1, ct, ch);   // the registers just consumed take tile t+1's chunk
+      }
+    }
+    __syncthreads();   // the previous tile's gather is done with zs
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int q = (wave + 4 * ct) * U3_HW + j;
+#pragma unroll
+      for (int it = 0; it < 3; ++it)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = it * 32 + acc_row(r, h);
+          if (row < T3_ROWS) zs[row * NPX + q] = acc[ct][it][r];
+        }
+    }
+    __syncthreads();
+    // gather: owned pixel (al, bl) -> its 4 classes x 3 channels; both column parities of a row pair are stored as
+    // one 32-B run
+    int n, a0, b0;
+    coords(t, n, a0, b0);
+    for (int idx = threadIdx.x; idx < R * U3_OW; idx += 256) {
+      const int al = idx / U3_OW, bl = idx - al * U3_OW;
+      const int a = a0 + al, b = b0 + bl;
+      if (a >= p.Hin || b >= p.Win) continue;
+#pragma unroll
+      for (int py = 0; py < 2; ++py) {
+        f32x4 o[2];
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+          float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+#pragma unroll
+          for (int ky = py; ky < 5; ky += 2)
+#pragma unroll
+            for (int kx = px; kx < 5; kx += 2) {
+              const int dy = (py + 2 - ky) / 2, dx = (px + 2 - kx) / 2;
+              const int q = (al + 1 + dy) * U3_HW + (bl + 1 + dx);
+              const int tap = ky * 5 + kx;
+              o0 += zs[(0 * 25 + tap) * NPX + q];
+              o1 += zs[(1 * 25 + tap) * NPX + q];
+              o2 += zs[(2 * 25 + tap) * NPX + q];
+            }
+          o[px] = f32x4{o0 + bias0, o1 + bias1, o2 + bias2, 0.f};
+        }
+        const int y = 2 * a + py, x = 2 * b;
+        float* dst = p.y + (((size_t)n * p.Hout + y) * p.Wout + x) * 4;
+        if (y < p.Hout) {
+          st4(dst, o[0]);
+          if (x + 1 < p.Wout) st4(dst + 4, o[1]);
+        }
+      }
+    }
+  }
+}
+
 // x6 weights for conv_up3: the pack_up3_kernel fragment order, each value split exactly into three bf16 planes
 __global__ void pack_up3_x6_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int Cin, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1813,8 +1956,20 @@ int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias,
   if (Cin % 16 != 0) return -2;
   ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
-  const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
-  hipLaunchKernelGGL((conv_up3_kernel<false, true>), dim3(tiles), dim3(256), 0, st, p);
+  auto persistent = [&](auto kern, int R) {
+    const int tiles = ((Win + U3_OW - 1) / U3_OW) * ((Hin + R - 1) / R) * N;
+    const int nblk = std::max(1, std::min(tiles, ica_cu_count()));
+    const int per = (tiles + nblk - 1) / nblk;
+    hipLaunchKernelGGL(kern, dim3((tiles + per - 1) / per), dim3(256), 0, st, p, per);
+  };
+  if (Cin == 128) {
+    persistent(conv_up3_x6p_kernel<8, 3>, u3_rows<3>());
+  } else if (Cin == 192) {
+    persistent(conv_up3_x6p_kernel<12, 2>, u3_rows<2>());
+  } else {
+    const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
+    hipLaunchKernelGGL((conv_up3_kernel<false, true>), dim3(tiles), dim3(256), 0, st, p);
+  }
   ICA_CHECK_LAUNCH();
   return 0;
 }

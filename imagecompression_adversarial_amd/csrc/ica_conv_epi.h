@@ -4,6 +4,9 @@
 // Reference anchors: anchors/utils.py:112-130 (conv / deconv geometry), utils/ops.py:58-97 (GDN).
 #pragma once
 #include "ica_common.h"
+#ifndef ICA_X6_RCP
+#define ICA_X6_RCP 0
+#endif
 
 enum {
   EPI_BIAS = 0,      // y = acc + bias
@@ -141,6 +144,14 @@ ICA_DEV void epi_params_to_lds(const ConvParams& p, f32x4* lp, int co_base) {
   }
 }
 
+// pixel (y, x) of an H x W activation plane -> its pixel index: row-major (PL = false) or parity-split (PL = true:
+// the four (y & 1, x & 1) sub-planes of (H/2) x (W/2) pixels one after another, H and W even)
+template <bool PL>
+ICA_DEV unsigned pix_index(int y, int x, int H, int W) {
+  if constexpr (PL) return ((unsigned)(((y & 1) * 2 + (x & 1)) * (H >> 1) + (y >> 1))) * (unsigned)(W >> 1) + (x >> 1);
+  else return (unsigned)y * W + x;
+}
+
 // --------------------------------------------------------------------------
 // Epilogue: acc[it] holds channels co_base + it*32 + acc_row(r,h) of pixel
 // (n, oy, ox) for this lane.  Register quad g (r = 4g..4g+3) of tile it is one
@@ -153,13 +164,13 @@ ICA_DEV void epi_params_to_lds(const ConvParams& p, f32x4* lp, int co_base) {
 // the three-plane gamma' pack of ica_pack_gdn_x6 (p.gp), fp32-accurate like the main loop of the x6 kernels.
 // LG: the epilogue parameters come from the block's epi_params_to_lds copy at lp (bf16 kernels); otherwise from
 // global memory
-template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false>
+template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false, bool PL = false>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
                            bool valid, int co_base, const f32x4* lp = nullptr) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int C4o = (p.Cout + 3) >> 2;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
-  const unsigned pix = valid ? ((unsigned)oy * p.Wout + ox) : 0u;
+  const unsigned pix = valid ? pix_index<PL>(oy, ox, p.Hout, p.Wout) : 0u;
   const size_t img = (size_t)C4o * plane;  // channel quads per image of every output-layout tensor
   // channel group c4 = u + h (u = co_base/4 + it*8 + 2g, wave-uniform): quad offset = vo + so(u)
   // (BF: every activation tensor of the epilogue is bf16 nChw4c, Img4T<true>)
@@ -272,6 +283,20 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // ica_pack_gdn_x6 splits, plane stride IT*IT*2048 bytes) and feeds all IT output tiles; the gamma' fragments
     // of round k+1 are issued before round k's MFMAs (4 independent accumulation chains hide their latency).
     const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, X6 ? IT * IT * 6144 : IT * IT * 4096);
+    // narrow x6: x^2 of every (tile, k-step) split into its three planes once, before the output tiles (the split
+    // per output tile and k-step repeated it IT times: ~1.4k VALU instructions per tile at IT = 4)
+    bf16x8 xs2[X6 == 2 ? IT : 1][2][3];
+    if constexpr (X6 == 2) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = acc[it][8 * s + j] * acc[it][8 * s + j];
+          split3x8(v, xs2[it][s]);
+        }
+    }
     f32x16 nx[X6 == 1 ? IT : 1];
     if constexpr (X6 == 1) {
       static_assert(!BF, "x6 epilogue: fp32 activations");
@@ -350,15 +375,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 #pragma unroll
           for (int i2 = 0; i2 < IT / 2; ++i2)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const int it = hb * (IT / 2) + i2;
-              float v[8];
-#pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] = acc[it][8 * s + j] * acc[it][8 * s + j];
-              bf16x8 xq[3];
-              split3x8(v, xq);
-              nacc = mfma_x6(ga[i2][s], xq, nacc);
-            }
+            for (int s = 0; s < 2; ++s) nacc = mfma_x6(ga[i2][s], xs2[hb * (IT / 2) + i2][s], nacc);
         }
       }
 #pragma unroll
@@ -510,9 +527,12 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const f32x4 yv = X6 ? yq[X6 ? it : 0][g] : IX.ld(vo_ld, ss), sv = X6 ? sq[X6 ? it : 0][g] : IS.ld(vo_ld, ss);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float sg = sv[e], xs = yv[e] / sg;
+            // x6: one v_rcp_f32 instead of two IEEE divisions (as gdn_bwd_x6_wide)
+            const float sg = sv[e], rs = X6 && ICA_X6_RCP ? __builtin_amdgcn_rcpf(sg) : 0.f;
+            const float xs = X6 && ICA_X6_RCP ? yv[e] * rs : yv[e] / sg;
             const float gx = acc[it][4 * g + e] * xs;
-            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
+            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg)
+                                                  : (X6 && ICA_X6_RCP ? (0.5f * gx) * rs : gx / (2.0f * sg));
             if constexpr (X6 == 1) tw[4 * (g & 1) + e] = tv;
             else tt[it][4 * g + e] = tv;
             float gs = acc[it][4 * g + e] * sg;
@@ -745,7 +765,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 // next round's loads a whole round = 1.5k cycles ahead), which halves the fragment traffic of two single-tile
 // epilogues and hides its L2 latency.  Requires IT*32 == Cout, co_base == 0, FX == 0.
 // --------------------------------------------------------------------------
-template <int IT, int EPI>
+template <int IT, int EPI, bool PL = false>
 ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, const int (&oy)[2],
                              const int (&ox)[2]) {
   static_assert(EPI == EPI_GDN || EPI == EPI_IGDN, "forward GDN epilogues only");
@@ -797,7 +817,7 @@ ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, c
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     if (oy[t] >= p.Hout || ox[t] >= p.Wout) continue;
-    const unsigned vo = h * plane + (unsigned)oy[t] * p.Wout + ox[t];
+    const unsigned vo = h * plane + pix_index<PL>(oy[t], ox[t], p.Hout, p.Wout);
 #pragma unroll
     for (int ct = 0; ct < IT; ++ct)
 #pragma unroll
@@ -813,6 +833,98 @@ ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, c
         const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
         if (p.save_s) SS.st(vo, ss, sv);
         Y.st(vo, ss, yv);
+      }
+  }
+}
+
+// --------------------------------------------------------------------------
+// The wide x6 GDN / IGDN backward epilogue (conv_epilogue<.., X6 = 1> with FX == 0, IT <= 4) in two halves, so that
+// a pipelined kernel can issue the saved (y, s) loads of a tile before its main loop:
+//   gdn_bwd_x6_load  : every (y, s) quad of the lane's pixel (a pixel outside the output reads past the descriptor:
+//                      0; its MFMA column is never stored)
+//   gdn_bwd_x6_wide  : the X6 = 1 arithmetic with the two IEEE divisions per element (x = y / s and, IGDN,
+//                      t = g x / (2 s)) replaced by one v_rcp_f32 (1 ulp): x = y rcp(s), t = 0.5 g x rcp(s).  The
+//                      divisions were ~20 of the epilogue's ~35 VALU instructions per element, as many cycles as the
+//                      kernel's MFMAs at one wave per SIMD; the x6 main loop's own error is ~17 ulps
+// --------------------------------------------------------------------------
+template <int IT, bool PL = false>
+ICA_DEV void gdn_bwd_x6_load(const ConvParams& p, int n, int oy, int ox, bool valid, f32x4 (&yq)[IT][4],
+                             f32x4 (&sq)[IT][4]) {
+  const int h = (threadIdx.x & 63) >> 5;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const Img4 IX(p.in_x, img, n), IS(p.in_s, img, n);
+  const unsigned vo = valid ? h * plane + pix_index<PL>(oy, ox, p.Hout, p.Wout) : 0x0FFFFFF0u;
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      yq[it][g] = IX.ld(vo, (unsigned)(it * 8 + 2 * g) * plane);
+      sq[it][g] = IS.ld(vo, (unsigned)(it * 8 + 2 * g) * plane);
+    }
+}
+
+template <int IT, int EPI, bool PL = false>
+ICA_DEV void gdn_bwd_x6_wide(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox, bool valid,
+                             const f32x4 (&yq)[IT][4], const f32x4 (&sq)[IT][4]) {
+  static_assert(EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD, "GDN backward epilogues only");
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const Img4 Y(p.y, img, n);
+  const unsigned vo = valid ? h * plane + pix_index<PL>(oy, ox, p.Hout, p.Wout) : 0u;
+  f32x16 xx[IT];
+  bf16x8 tq[IT][2][3];
+  float tw[8];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 yv = yq[it][g], sv = sq[it][g];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sg = sv[e], rs = __builtin_amdgcn_rcpf(sg), xs = yv[e] * rs;
+        const float gx = acc[it][4 * g + e] * xs;
+        tw[4 * (g & 1) + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : (0.5f * gx) * rs;
+        float gs = acc[it][4 * g + e] * sg;
+        float x2 = 2.0f * xs;
+        asm volatile("" : "+v"(gs), "+v"(x2));
+        acc[it][4 * g + e] = gs;
+        xx[it][4 * g + e] = x2;
+      }
+      if (g & 1) split3x8(tw, tq[it][g >> 1]);
+    }
+  __builtin_amdgcn_sched_barrier(0);
+  const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+  f32x16 ux[IT];
+#pragma unroll
+  for (int jt = 0; jt < IT; ++jt) ux[jt] = f32x16{0};
+  bf16x8 ga[2][IT][3];
+  auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
+#pragma unroll
+    for (int jt = 0; jt < IT; ++jt)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        a[jt][q] = ld_bf8(grs, lane * 16, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+  };
+  ldg(ga[0], 0);
+#pragma unroll
+  for (int k = 0; k < 2 * IT; ++k) {
+    if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int jt = 0; jt < IT; ++jt) ux[jt] = mfma_x6(ga[k & 1][jt], tq[k >> 1][k & 1], ux[jt]);
+  }
+  if (valid) {
+#pragma unroll
+    for (int jt = 0; jt < IT; ++jt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + xx[jt][4 * g + e] * ux[jt][4 * g + e];
+        Y.st(vo, (unsigned)(jt * 8 + 2 * g) * plane, v);
       }
   }
 }

@@ -8,8 +8,8 @@ scales: "t100a" (10 branch flips into the cheap branch) and "t100b" (hovers at t
 Checks and stated tolerances:
   * the lr table (MultiStepLR stepped every steps//3, milestones 1/2/3 -> drops at i = 0, 33, 66) equals the
     reference's, value for value;
-  * CPU oracle: identical branch sequence over all 100 steps, loss_i rel <= 1e-4, final noise max rel <= 5e-2 with
-    99.9 % <= 5e-3 (another CPU's fp32 reduction order, amplified by Adam; ~1e-6 on one platform), eval metrics
+  * CPU oracle: identical branch sequence over all 100 steps, loss_i rel <= 1e-4, final noise within NOISE_MAX /
+    NOISE_P999 (another CPU's fp32 reduction order, amplified by Adam; 0 on the generating platform), eval metrics
     rel <= 1e-3;
   * HIP path (-m gpu), on BOTH operand paths (fp32 MFMA and the default x6 = fp32-accurate bf16x6): pre-eval
     latents within 1e-5 of max|y| with rounding differences only at near-ties, the target equal to the reference
@@ -18,10 +18,11 @@ Checks and stated tolerances:
     asserted as the bound (the branch at loss_i ~ -noise is discontinuous, so an fp32 reduction-order difference
     may flip a late step; the assertion message carries both branch strings); loss_i per step rel <= 1e-3 while
     the sequences agree; up to the first divergence the noise itself against the reference's
-    (tests/golden/traj100_snap.npz, same run): at the snapshot steps max rel <= 5e-2 with 99.9 % <= 5e-3, and per
-    step the fingerprints sum|noise| / sum noise^2 / <noise, pattern> rel <= 1e-2 of their scale; the final
-    noise (when all 100 agree) max rel <= 5e-2 with 99.9 % <= 5e-3 (for scale: the same algorithm in fp64
-    diverges from the fp32 reference's branch sequence at step 32 / 40 and ends O(1) away); final mse_in within
+    (tests/golden/traj100_snap.npz, same run): at the snapshot steps within NOISE_MAX / NOISE_P999 (the spread of
+    18 fp32 re-evaluations of the reference algorithm, x1.25), and per step the fingerprints sum|noise| /
+    sum noise^2 / <noise, pattern> rel <= 1e-2 of their scale; the final noise (when all 100 agree) within the
+    same bounds (for scale: the same algorithm in fp64 diverges from the fp32 reference's branch sequence at step
+    32 / 40 and ends O(1) away); final mse_in within
     10 % of the reference's, VI within 1 dB, |noise_c| <= eps and im_in in [0, 1] exactly.
 Measured on MI355X (round 3): both paths keep the reference's branch sequence for all 100 steps on both runs.
 x6 ends further from the reference noise on t100b (max 4.8e-2, p99.9 1.3e-3; fp32 1.6e-2 / 3.9e-4) although its
@@ -41,6 +42,11 @@ from tests.conftest import REPO
 FIX = os.path.join(REPO, "tests", "golden", "traj100.npz")
 SNAP = os.path.join(REPO, "tests", "golden", "traj100_snap.npz")
 TAGS = ("t100a", "t100b")
+# Noise bounds, relative to max|noise_ref|: what fp32 rounding alone does to this trajectory.  18 fp32 re-evaluations
+# of the reference algorithm on the CPU oracle (1 thread instead of 8, weights or the image moved by +-1 ulp;
+# scripts/traj100_spread.py -> profiles/r03/traj100_spread.txt) keep all 100 branches but end up to 4.77e-2 (max)
+# and 1.41e-2 (99.9th percentile) away from the reference's final noise; the bounds are 1.25x those.
+NOISE_MAX, NOISE_P999 = 6e-2, 1.8e-2
 # first step whose branch differs from the reference's (100 = none), as achieved on MI355X by each path
 DIV_MIN = {("t100a", "fp32"): 100, ("t100b", "fp32"): 100, ("t100a", "x6"): 100, ("t100b", "x6"): 100}
 
@@ -89,17 +95,16 @@ def test_oracle_traj100_vs_reference(t100, tag):
     li = np.array([float(d["loss_i"][0]) for d in rec])
     assert np.abs(li - t100[f"{tag}_loss_i"]).max() <= 1e-4 * np.abs(t100[f"{tag}_loss_i"]).max()
     # same-platform runs agree to ~1e-6; another CPU (ISA / thread split of the conv reductions) reorders fp32 sums
-    # and Adam's 1/sqrt(v) amplifies that where |g| ~ eps, so the bound is the HIP test's (max 5e-2, p99.9 5e-3)
-    ref_noise = t100[f"{tag}_noise"]
-    d = np.abs(r.noise.numpy() - ref_noise) / np.abs(ref_noise).max()
-    assert d.max() <= 5e-2 and float((d <= 5e-3).mean()) >= 0.999
+    # and Adam's 1/sqrt(v) amplifies that where |g| ~ eps, so the bound is the calibrated fp32 spread (NOISE_MAX / NOISE_P999)
+    mx, p999 = _noise_close(r.noise.numpy(), t100[f"{tag}_noise"])
+    assert mx <= NOISE_MAX and p999 <= NOISE_P999, (mx, p999)
     assert abs(float(r.eval.mse_in[0]) - float(t100[f"{tag}_mse_in"])) <= 1e-3 * float(t100[f"{tag}_mse_in"])
     assert abs(float(r.eval.mse_out[0]) - float(t100[f"{tag}_mse_out"])) <= 1e-3 * float(t100[f"{tag}_mse_out"])
 
 
 def _noise_close(got, ref):
     d = np.abs(got - ref) / np.abs(ref).max()
-    return float(d.max()), float((d <= 5e-3).mean()), float(np.quantile(d, 0.999))
+    return float(d.max()), float(np.quantile(d, 0.999))
 
 
 @pytest.mark.gpu
@@ -169,17 +174,16 @@ def test_hip_traj100_vs_reference(t100, tag, precision):
         assert (rel <= 1e-2).all(), (i, fp[i].tolist(), ref_fp[i].tolist())
     for k, i in enumerate(snap_steps):
         if i < div:
-            mx, frac, p999 = _noise_close(snaps[i], snap[f"{tag}_snap"][k])
+            mx, p999 = _noise_close(snaps[i], snap[f"{tag}_snap"][k])
             print(f"{tag}/{precision}: noise after step {i}: rel diff max {mx:.2e}, p99.9 {p999:.2e}")
-            assert mx <= 5e-2 and frac >= 0.999, (i, mx, frac)
+            assert mx <= NOISE_MAX and p999 <= NOISE_P999, (i, mx, p999)
     if div == 100:
-        # Adam's 1/sqrt(v) amplifies fp32 ordering differences where |g| ~ eps: max <= 5e-2 and 99.9 % of the
-        # elements <= 5e-3, relative to max|noise|.  Scale of what fp32 rounding alone does to this chaotic
-        # loop: the SAME algorithm in fp64 leaves the fp32 reference's branch sequence at step 32 (t100a) / 40
-        # (t100b) and ends O(1) away (max 1.3 / 1.5, p99.9 0.95 / 0.99 of max|noise|; measured here)
-        mx, frac, p999 = _noise_close(loop.noise.cpu().numpy(), t100[f"{tag}_noise"])
+        # Adam's 1/sqrt(v) amplifies fp32 ordering differences where |g| ~ eps (NOISE_MAX / NOISE_P999 above; for
+        # scale: the SAME algorithm in fp64 leaves the fp32 reference's branch sequence at step 32 (t100a) / 40
+        # (t100b) and ends O(1) away, max 1.3 / 1.5, p99.9 0.95 / 0.99 of max|noise|)
+        mx, p999 = _noise_close(loop.noise.cpu().numpy(), t100[f"{tag}_noise"])
         print(f"{tag}/{precision}: final noise rel diff max {mx:.2e}, p99.9 {p999:.2e}")
-        assert mx <= 5e-2 and frac >= 0.999, (mx, frac)
+        assert mx <= NOISE_MAX and p999 <= NOISE_P999, (mx, p999)
     res = evaluate(kern, loop.im_in, loop.im_s, loop.output_s, msssim=False)
     mse_in, mse_out = float(res[3][0]), float(res[4][0])
     assert abs(mse_in - float(t100[f"{tag}_mse_in"])) <= 0.1 * float(t100[f"{tag}_mse_in"])
