@@ -35,7 +35,7 @@ _SIGS = {
     "ica_pack_gdn_x6_size": [_i],
     "ica_pack_up3_bf16": [_p, _p, _i, _p],
     "ica_pack_up3_x6": [_p, _p, _i, _p],
-    "ica_conv_up3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_conv_up3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
@@ -117,7 +117,7 @@ class ConvArgs(C.Structure):
     _fields_ = ([(n, C.c_void_p) for n in ("x", "y", "wp", "bias", "gp", "beta", "save_x", "save_s", "in_x", "in_s",
                                             "save_t", "res", "mask")]
                 + [(n, C.c_int) for n in ("N", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kind", "KS", "S", "epi",
-                                           "it", "fill_mode", "ps", "prec")])
+                                           "it", "fill_mode", "ps", "prec", "layout")])
 
 
 _lib = None

@@ -114,7 +114,9 @@ class _TransformFn(torch.autograd.Function):
             raise NotImplementedError(f"{type(module).__name__}: parameter gradients are computed for the bmshj2018 "
                                       "g_a / g_s only; freeze this transform with requires_grad_(False)")
         x4 = K.to_nc4(x.detach().contiguous())
-        out4, saved = ex.forward(x4, save=need_x or need_w)
+        # parameter gradients read the saved activations row-major (the wgrad kernels)
+        kw = {"split": False} if need_w and isinstance(ex, (E.Analysis, E.Synthesis)) else {}
+        out4, saved = ex.forward(x4, save=need_x or need_w, **kw)
         ctx.ex, ctx.saved, ctx.cin, ctx.module = ex, saved, x.shape[1], module
         ctx.x4 = x4 if need_w else None
         ctx.need_x, ctx.need_w = need_x, need_w

@@ -1284,7 +1284,8 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int 
     const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
     const int iy = a0 - 1 + wave + 4 * ct, ix = b0 - 1 + j;
     const bool ok = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const unsigned o0 = ok ? ((unsigned)(4 * ch + 2 * h) * plane + (unsigned)iy * p.Win + ix) * 16u : 0xFFFFFFF0u;
+    const unsigned o0 =
+        ok ? ((unsigned)(4 * ch + 2 * h) * plane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u : 0xFFFFFFF0u;
     xa[ct][ch][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o0, 0, 0));
     xa[ct][ch][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? o0 + plane * 16u : 0xFFFFFFF0u,
                                                                                      0, 0));
@@ -1834,7 +1835,8 @@ typedef struct ica_conv_args {
   const float* mask;
   int N, Cin, Hin, Win, Cout, Hout, Wout;
   int kind, KS, S, epi, it, fill_mode, ps;
-  int prec; /* 0 fp32 operands, 1 bf16 operands (fp32 accumulate) */
+  int prec;   /* 0 fp32 operands, 1 bf16 operands (fp32 accumulate), 2 bf16x6 (fp32-accurate) */
+  int layout; /* parity-split tensors: 1 = x, 2 = the output-layout tensors (ConvParams::pl) */
 } ica_conv_args;
 
 // Channel tile (IT = number of 32-channel MFMA row tiles per wave) the conv
@@ -1952,10 +1954,13 @@ int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t st) {
 }
 
 int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
-                    hipStream_t st) {
+                    int layout, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
+  if (layout & ~PL_IN) return -4;   // the 3-channel output is the image: row-major
+  if ((layout & PL_IN) && ((Hin | Win) & 1 || (Cin != 128 && Cin != 192))) return -2;
   ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
+  p.pl = layout;
   auto persistent = [&](auto kern, int R) {
     const int tiles = ((Win + U3_OW - 1) / U3_OW) * ((Hin + R - 1) / R) * N;
     const int nblk = std::max(1, std::min(tiles, ica_cu_count()));
@@ -2074,8 +2079,13 @@ int ica_conv_up(const float* x, float* y, const float* wp, const float* bias, in
 int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   ConvParams p{a->x,    a->y,    a->wp,   a->bias, a->gp,   a->beta, a->save_x, a->save_s, a->in_x, a->in_s,
                a->N,    a->Cin,  a->Hin,  a->Win,  a->Cout, a->Hout, a->Wout,   a->save_t, a->res,  a->mask,
-               a->fill_mode, a->ps, a->prec};
+               a->fill_mode, a->ps, a->prec, a->layout};
   if (a->prec != 0 && a->prec != 1 && a->prec != 2) return -4;
+  // parity-split tensors: x6 k5 s2 launches only (ica_conv_x6_dispatch checks the rest), even planes
+  if (a->layout & ~(PL_IN | PL_OUT)) return -4;
+  if (a->layout && (a->prec != 2 || a->KS != 5 || a->S != 2)) return -4;
+  if (((a->layout & PL_IN) && ((a->Hin | a->Win) & 1)) || ((a->layout & PL_OUT) && ((a->Hout | a->Wout) & 1)))
+    return -2;
   const int it = resolve_it(a->Cout, a->it);
   if (a->epi >= EPI_GDN && a->epi <= EPI_IGDN_BWD && a->Cout != it * 32) return -4;
   if (a->ps && (a->Cout % 16 != 0 || !(a->epi == EPI_BIAS || a->epi == EPI_RELU || a->epi == EPI_LRELU))) return -4;

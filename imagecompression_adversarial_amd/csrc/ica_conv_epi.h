@@ -51,7 +51,10 @@ struct ConvParams {
                       //    bf16 packs (ica_pack_conv_weight_bf16 / ica_pack_gdn_bf16)
                       // 2: fp32-accurate bf16x6 operands (ica_conv_x6.hip; wp = ica_pack_conv_weight_x6, fp32
                       //    activations and epilogues, gp = the fp32 gamma' pack)
+  int pl;             // parity-split pixel order (pix_at): PL_IN = x, PL_OUT = every output-layout tensor (y,
+                      // save_x / save_s, in_x / in_s, save_t, res); x6 k5 s2 kernels and the x6 conv_up3 only
 };
+enum { PL_IN = 1, PL_OUT = 2 };
 
 // v -> (hi, mid, lo) bf16 quads, each stage round-to-nearest-even on the residual (exact: hi + mid + lo == v)
 ICA_DEV void split3(f32x4 v, u32x2& hi, u32x2& mid, u32x2& lo) {
@@ -144,12 +147,13 @@ ICA_DEV void epi_params_to_lds(const ConvParams& p, f32x4* lp, int co_base) {
   }
 }
 
-// pixel (y, x) of an H x W activation plane -> its pixel index: row-major (PL = false) or parity-split (PL = true:
-// the four (y & 1, x & 1) sub-planes of (H/2) x (W/2) pixels one after another, H and W even)
-template <bool PL>
-ICA_DEV unsigned pix_index(int y, int x, int H, int W) {
-  if constexpr (PL) return ((unsigned)(((y & 1) * 2 + (x & 1)) * (H >> 1) + (y >> 1))) * (unsigned)(W >> 1) + (x >> 1);
-  else return (unsigned)y * W + x;
+// pixel (y, x) of an H x W activation plane -> its pixel index: row-major, or parity-split (split: the four
+// (y & 1, x & 1) sub-planes of (H/2) x (W/2) pixels one after another, H and W even; ConvParams::pl).  A conv_up
+// parity class then owns a dense sub-plane, so its 16-B stores (and the GDN-backward epilogue's saved (y, s) loads)
+// fill whole cache lines instead of every other 16 B of each line
+ICA_DEV unsigned pix_at(int y, int x, int H, int W, bool split) {
+  return split ? ((unsigned)((((y & 1) << 1) | (x & 1)) * (H >> 1) + (y >> 1))) * (unsigned)(W >> 1) + (x >> 1)
+               : (unsigned)y * W + x;
 }
 
 // --------------------------------------------------------------------------
@@ -164,13 +168,13 @@ ICA_DEV unsigned pix_index(int y, int x, int H, int W) {
 // the three-plane gamma' pack of ica_pack_gdn_x6 (p.gp), fp32-accurate like the main loop of the x6 kernels.
 // LG: the epilogue parameters come from the block's epi_params_to_lds copy at lp (bf16 kernels); otherwise from
 // global memory
-template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false, bool PL = false>
+template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
                            bool valid, int co_base, const f32x4* lp = nullptr) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int C4o = (p.Cout + 3) >> 2;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
-  const unsigned pix = valid ? pix_index<PL>(oy, ox, p.Hout, p.Wout) : 0u;
+  const unsigned pix = valid ? pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u;
   const size_t img = (size_t)C4o * plane;  // channel quads per image of every output-layout tensor
   // channel group c4 = u + h (u = co_base/4 + it*8 + 2g, wave-uniform): quad offset = vo + so(u)
   // (BF: every activation tensor of the epilogue is bf16 nChw4c, Img4T<true>)
@@ -765,7 +769,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
 // next round's loads a whole round = 1.5k cycles ahead), which halves the fragment traffic of two single-tile
 // epilogues and hides its L2 latency.  Requires IT*32 == Cout, co_base == 0, FX == 0.
 // --------------------------------------------------------------------------
-template <int IT, int EPI, bool PL = false>
+template <int IT, int EPI>
 ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, const int (&oy)[2],
                              const int (&ox)[2]) {
   static_assert(EPI == EPI_GDN || EPI == EPI_IGDN, "forward GDN epilogues only");
@@ -817,7 +821,7 @@ ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, c
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     if (oy[t] >= p.Hout || ox[t] >= p.Wout) continue;
-    const unsigned vo = h * plane + pix_index<PL>(oy[t], ox[t], p.Hout, p.Wout);
+    const unsigned vo = h * plane + pix_at(oy[t], ox[t], p.Hout, p.Wout, p.pl & PL_OUT);
 #pragma unroll
     for (int ct = 0; ct < IT; ++ct)
 #pragma unroll
@@ -847,14 +851,14 @@ ICA_DEV void gdn_fwd_x6_pair(const ConvParams& p, f32x16 (&acc)[2][IT], int n, c
 //                      divisions were ~20 of the epilogue's ~35 VALU instructions per element, as many cycles as the
 //                      kernel's MFMAs at one wave per SIMD; the x6 main loop's own error is ~17 ulps
 // --------------------------------------------------------------------------
-template <int IT, bool PL = false>
+template <int IT>
 ICA_DEV void gdn_bwd_x6_load(const ConvParams& p, int n, int oy, int ox, bool valid, f32x4 (&yq)[IT][4],
                              f32x4 (&sq)[IT][4]) {
   const int h = (threadIdx.x & 63) >> 5;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
   const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
   const Img4 IX(p.in_x, img, n), IS(p.in_s, img, n);
-  const unsigned vo = valid ? h * plane + pix_index<PL>(oy, ox, p.Hout, p.Wout) : 0x0FFFFFF0u;
+  const unsigned vo = valid ? h * plane + pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0x0FFFFFF0u;
 #pragma unroll
   for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -864,7 +868,7 @@ ICA_DEV void gdn_bwd_x6_load(const ConvParams& p, int n, int oy, int ox, bool va
     }
 }
 
-template <int IT, int EPI, bool PL = false>
+template <int IT, int EPI>
 ICA_DEV void gdn_bwd_x6_wide(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox, bool valid,
                              const f32x4 (&yq)[IT][4], const f32x4 (&sq)[IT][4]) {
   static_assert(EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD, "GDN backward epilogues only");
@@ -872,7 +876,7 @@ ICA_DEV void gdn_bwd_x6_wide(const ConvParams& p, f32x16 (&acc)[IT], int n, int 
   const unsigned plane = (unsigned)p.Hout * p.Wout;
   const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
   const Img4 Y(p.y, img, n);
-  const unsigned vo = valid ? h * plane + pix_index<PL>(oy, ox, p.Hout, p.Wout) : 0u;
+  const unsigned vo = valid ? h * plane + pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u;
   f32x16 xx[IT];
   bf16x8 tq[IT][2][3];
   float tw[8];

@@ -26,9 +26,6 @@
 
 #include "ica_conv_epi.h"
 
-#ifndef ICA_EXP_PLANAR
-#define ICA_EXP_PLANAR false
-#endif
 namespace {
 
 constexpr int X6_PT = 2;                 // 32-pixel tiles per wave
@@ -41,20 +38,13 @@ constexpr int xd_th() { return 4 * PT; }
 
 // --------------------------------------------------------------------------------------------------------------
 // conv_down_x6: weights [plane][cb][chunk][tap][it][lane] bf16x8 (plane stride ps fragments)
-//
-// The input patch of a 16-channel chunk is staged RAW (fp32, 81 KB at PT = 2) in one of two LDS buffers, and each B
-// operand is split into its three bf16 planes when it is read (a step ahead of its MFMAs, ~2 VALU instructions per
-// MFMA gap).  The next chunk's patch streams into the other buffer during the current chunk's 25 taps (four batches,
-// each loaded at tap 6k and written to LDS at tap 6k + 5), so one barrier per chunk is all that remains of the fill
-// (the single three-plane buffer, 122 KB, was refilled between two barriers at every chunk boundary: ~25 % of the
-// main loop).
 // --------------------------------------------------------------------------------------------------------------
 template <int IT, int EPI, int PT = X6_PT>
 __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long ps) {
   constexpr int KS = 5, S = 2, PAD = 2, KK = 25, TW = XD_TW, TH = xd_th<PT>();
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;
-  constexpr int NF = (4 * PLANE + 255) / 256, NBT = 4, NB = (NF + NBT - 1) / NBT;   // fill items per thread, batches
-  __shared__ f32x4 patch[2][4 * PLANE];                                              // [buffer][quad][pixel] fp32
+  constexpr int NF = (4 * PLANE + 255) / 256, NB = (NF + 1) / 2;  // fill items per thread, in two batches
+  __shared__ f32x4 patch[3 * 2 * PLANE];                          // [plane][half][pixel]: 8 channels as bf16
   const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
   int bid, cb;
   xcd_block<true>(bid, cb);
@@ -73,26 +63,36 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
     for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
 
   // patch fill: 16-B buffer loads (32-bit offsets into this image; padding and channel quads past Cin read out of
-  // the descriptor's range and return zeros), written to LDS as they are
+  // the descriptor's range and return zeros), split into the three planes.  The first batch is issued before the
+  // barrier that ends the previous chunk's reads.
   const unsigned xplane = (unsigned)p.Hin * p.Win;
   const __amdgpu_buffer_rsrc_t xr =
       uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
-  auto batch = [&](int ch, int k, f32x4 (&v)[NB]) __attribute__((always_inline)) {
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  auto batch = [&](int ch, int i0, f32x4 (&v)[NB]) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int e = threadIdx.x + 256 * (k * NB + i);
+      const int e = threadIdx.x + 256 * (i0 + i);
       const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
       const int iy = iy0 + pr, ix = ix0 + pc, c4 = ch * 4 + q;
-      const bool ok = k * NB + i < NF && e < 4 * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      const bool ok = i0 + i < NF && e < 4 * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
       v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
     }
   };
-  auto put = [&](int buf, int k, const f32x4 (&v)[NB]) __attribute__((always_inline)) {
+  auto put = [&](int i0, const f32x4 (&v)[NB]) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int e = threadIdx.x + 256 * (k * NB + i);
-      if (k * NB + i < NF && e < 4 * PLANE) patch[buf][e] = v[i];
+      const int e = threadIdx.x + 256 * (i0 + i);
+      if (i0 + i < NF && e < 4 * PLANE) {
+        const int q = e / PLANE, pix = e - q * PLANE;
+        u32x2 a, b, c;
+        split3(v[i], a, b, c);
+        const int ent = (q >> 1) * PLANE + pix;
+        p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
+        p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+        p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+      }
     }
   };
   const int total = nch * KK;
@@ -106,82 +106,50 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
 #pragma unroll
       for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
   };
-  // raw B operands of step (buffer, tap): channels 8h..8h+7 of the lane's patch pixel, two quads per pixel tile
-  auto ldb = [&](f32x4 (&r)[PT][2], int buf, int tap) __attribute__((always_inline)) {
+  // one (chunk, tap) step: the next step's fragments are issued first, a whole step (48 MFMAs) ahead of their use
+  // (the barrier keeps the scheduler from sinking them to their first use); hook() issues patch loads after them
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g, int tap, auto hook) __attribute__((always_inline)) {
+    ldw(nxt, g + 1);
+    hook();
+    __builtin_amdgcn_sched_barrier(0);
     const int ky = tap / 5, kx = tap - ky * 5;
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
-      const int o = (S * (wave * PT + t) + ky) * PC + S * j + kx;
-      r[t][0] = patch[buf][(2 * h) * PLANE + o];
-      r[t][1] = patch[buf][(2 * h + 1) * PLANE + o];
+      const int o = h * PLANE + (S * (wave * PT + t) + ky) * PC + S * j + kx;
+      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], b, acc[t][it]);
     }
   };
-  auto split = [&](const f32x4 (&r)[PT][2], bf16x8 (&b)[PT][3]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const float v[8] = {r[t][0][0], r[t][0][1], r[t][0][2], r[t][0][3], r[t][1][0], r[t][1][1], r[t][1][2], r[t][1][3]};
-      split3x8(v, b[t]);
-    }
-  };
-  f32x4 fv[NB];
-  // prologue: chunk 0 into buffer 0
-#pragma unroll
-  for (int k = 0; k < NBT; ++k) {
-    batch(0, k, fv);
-    put(0, k, fv);
-  }
-  __syncthreads();
-  bf16x8 fa[IT][3], fb[IT][3];
-  ldw(fa, 0);
-  f32x4 raw[PT][2];
-  bf16x8 bc[PT][3];
-  ldb(raw, 0, 0);
-  split(raw, bc);
-  // one (chunk, tap) step: the next step's weight fragments and raw B operands are issued first (the sched barrier
-  // keeps the scheduler from sinking them to their first use), then this step's MFMAs, with the next operand's
-  // split free to interleave with them
-  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g, int buf, int tap, int nbuf, int ntap,
-                  auto hook) __attribute__((always_inline)) {
-    ldw(nxt, g + 1);
-    ldb(raw, nbuf, ntap);
-    hook();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int t = 0; t < PT; ++t)
-#pragma unroll
-      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(cur[it], bc[t], acc[t][it]);
-    split(raw, bc);
-  };
-  // chunk ch from buffer ch & 1; chunk ch + 1 streams into the other buffer: batch k is loaded at tap 6k and written
-  // at tap 6k + 5 (a rolled loop over tap pairs: unrolled taps multiplied the scalar offsets and the live ranges);
-  // the last tap's "next" operand is read after the barrier that publishes the next buffer
+  auto none = []() {};
+  // the next chunk's patch is loaded into registers during the last KK - TPF taps of the current one (both
+  // batches, a straight-line tail so the waits stay exact) and staged into LDS between two barriers at the chunk
+  // boundary: only the split and the LDS writes remain exposed (the fill's HBM latency was ~30 % of the loop)
+  constexpr int TPF = 20;
+  f32x4 v1[NB], v2[NB];
   auto chunk = [&](bf16x8 (&fa)[IT][3], bf16x8 (&fb)[IT][3], int ch) __attribute__((always_inline)) {
-    const int buf = ch & 1, nb = buf ^ 1, g0 = ch * KK;
-    const bool more = ch + 1 < nch;
-#pragma unroll 1
-    for (int tp = 0; tp < KK - 1; tp += 2) {
-      step(fa, fb, g0 + tp, buf, tp, buf, tp + 1, [&]() __attribute__((always_inline)) {
-        if (more && tp % 6 == 0) batch(ch + 1, tp / 6, fv);
-      });
-      step(fb, fa, g0 + tp + 1, buf, tp + 1, buf, tp + 2, [&]() __attribute__((always_inline)) {
-        if (more && tp % 6 == 4) put(nb, tp / 6, fv);
-      });
-    }
-    // last tap: the MFMAs of tap 24, then the barrier, then the next chunk's first operand
-    ldw(fb, g0 + KK);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int t = 0; t < PT; ++t)
-#pragma unroll
-      for (int it = 0; it < IT; ++it) acc[t][it] = mfma_x6(fa[it], bc[t], acc[t][it]);
+    batch(ch, NB, v2);
     __syncthreads();
-    if (more) {
-      ldb(raw, nb, 0);
-      split(raw, bc);
+    put(0, v1);
+    put(NB, v2);
+    __syncthreads();
+    const int g0 = ch * KK, cn = min(ch + 1, nch - 1);
+#pragma unroll 1
+    for (int tp = 0; tp < TPF; tp += 2) {
+      step(fa, fb, g0 + tp, tp, none);
+      step(fb, fa, g0 + tp + 1, tp + 1, none);
+    }
+    step(fa, fb, g0 + TPF, TPF, [&]() { batch(cn, 0, v1); });
+#pragma unroll
+    for (int tp = TPF + 1; tp < KK; ++tp) {
+      if ((tp - TPF) & 1) step(fb, fa, g0 + tp, tp, none);
+      else step(fa, fb, g0 + tp, tp, none);
     }
   };
-  static_assert(KK % 2 == 1, "chunk parity: a chunk starting on fa ends with the next fragments in fb");
-  static_assert(NBT * 6 == KK - 1, "four 6-tap fill groups, then the last tap");
+  static_assert(TPF % 2 == 0 && KK % 2 == 1, "chunk parity: a chunk starting on fa ends with the next fragments in fb");
+  bf16x8 fa[IT][3], fb[IT][3];
+  batch(0, 0, v1);
+  ldw(fa, 0);
   int ch = 0;
 #pragma unroll 1
   for (; ch + 1 < nch; ch += 2) {
@@ -501,7 +469,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
         const int q = e / XU_PLANE, rem = e - q * XU_PLANE, pr = rem / XU_PC, pc = rem - pr * XU_PC;
         const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
         const bool ok = e < TOT && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-        const unsigned vo = ((unsigned)(grp * NQ + q) * xplane + (unsigned)iy * p.Win + ix) * 16u;
+        const unsigned vo = ((unsigned)(grp * NQ + q) * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
         v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
       }
 #pragma unroll
@@ -540,13 +508,12 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
     if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
       const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
       const int ox[2] = {2 * (b0 + b_rel) + PX, 2 * (b0 + b_rel) + PX};
-      gdn_fwd_x6_pair<IT, EPI, ICA_EXP_PLANAR>(p, acc, n, oy, ox);
+      gdn_fwd_x6_pair<IT, EPI>(p, acc, n, oy, ox);
     } else {
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
         const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-        conv_epilogue<IT, EPI, 0, false, 1, false, ICA_EXP_PLANAR>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout,
-                                                                   cb * IT * 32);
+        conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
       }
     }
   };
@@ -634,7 +601,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_small_x6_kernel(ConvParams p
       const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
       const int iy = iy0 + pr, ix = ix0 + pc, c4 = ch * 4 + q;
       const bool ok = e < 4 * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      const unsigned vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
       v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
     }
     __syncthreads();
@@ -737,7 +704,7 @@ __global__ __launch_bounds__(256, 2) void conv_up_small_x6_kernel(ConvParams p, 
         const int q = e / XSU_PLANE, rem = e - q * XSU_PLANE, pr = rem / XSU_PC, pc = rem - pr * XSU_PC;
         const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
         const bool ok = e < TOT && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-        const unsigned vo = ((unsigned)q * xplane + (unsigned)iy * p.Win + ix) * 16u;
+        const unsigned vo = ((unsigned)q * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
         v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
       }
 #pragma unroll
@@ -991,6 +958,7 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
     if (p.Hout * 2 != p.Hin + (p.Hin & 1) || p.Wout * 2 != p.Win + (p.Win & 1)) return -2;
     if (p.Cin <= 4) {   // RGB-sized input: the PixelUnshuffle(2) k3 view (wp from the rearranged weight)
       if (it != 4) return -3;
+      if (p.pl & PL_IN) return -2;   // the image side stays row-major
       switch (epi) {
         case EPI_BIAS: return launch_rgb_x6<4, EPI_BIAS>(p, st);
         case EPI_GDN: return launch_rgb_x6<4, EPI_GDN>(p, st);

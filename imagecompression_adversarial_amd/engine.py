@@ -25,6 +25,26 @@ def _P(sd, prefix, name):
     return sd[f"{prefix}.{name}" if prefix else name]
 
 
+class Saved(list):
+    """The per-layer (y, s) pairs a forward saves for its backward, and whether the inner levels were stored
+    parity-split (the backward must address them the same way)."""
+
+    def __init__(self, items=(), split=False, exact=True):
+        super().__init__(items)
+        self.split = split
+        self.exact = exact   # every level exactly halves the one above (input sides multiples of 16)
+
+
+def _lay(split, inp, out):
+    return (K.LAYOUT_IN if split and inp else 0) | (K.LAYOUT_OUT if split and out else 0)
+
+
+def _split_capable(convs, N):
+    """Parity-split inner levels (L1-L3 of the k5 s2 stacks): every launch touching them runs an x6 kernel (the
+    only kernels that address that order), the 3-channel end on the x6 conv_up3 (N = 128 / 192)."""
+    return N in (128, 192) and all(c.fwd_prec == K.PREC_X6 and c.bwd_prec == K.PREC_X6 for c in convs)
+
+
 class Analysis:
     """g_a = conv(3,N)-GDN-conv(N,N)-GDN-conv(N,N)-GDN-conv(N,M), all k5 s2."""
 
@@ -38,29 +58,41 @@ class Analysis:
                                    it_fwd=g6 if i < 6 else 0, it_bwd=g6 if i > 0 else 0)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
+        self.split = _split_capable(self.convs, self.N)
 
-    def forward(self, x4, save=False):
-        h, C, saved = x4, 3, []
+    def forward(self, x4, save=False, split=None):
+        """split: store the inner levels L1-L3 parity-split (default: when every launch runs x6 and every inner
+        level has even sides; the transform's output y and its input gradient stay row-major either way)."""
+        H, W = x4.shape[2], x4.shape[3]
+        sides = [((H + (1 << k) - 1) >> k, (W + (1 << k) - 1) >> k) for k in (1, 2, 3)]
+        sp = (self.split if split is None else split) and all(a % 2 == 0 and b % 2 == 0 for a, b in sides)
+        h, C, saved = x4, 3, Saved(split=sp, exact=H % 16 == 0 and W % 16 == 0)
         for i in range(3):
             p = self.convs[i]
             h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.gdns[i], save,
-                                    tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd)
+                                    tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd,
+                                    layout=_lay(sp, i > 0, True))
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
         y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.6.fwd",
-                              prec=p.fwd_prec)
+                              prec=p.fwd_prec, layout=_lay(sp, True, False))
         return y, saved
 
     def backward(self, gy4, saved):
+        if not getattr(saved, "exact", True):
+            # the input gradients are 2x transposed convs: an odd level (sides not multiples of 16) has no
+            # exact transpose here (the attack pads its images to multiples of 64, coder.read_image)
+            raise ValueError("g_a input gradient: image sides must be multiples of 16")
+        sp = getattr(saved, "split", False)
         g, C = gy4, self.M
         for i in (3, 2, 1):
             g, _, _ = K.conv_up(g, C, self.convs[i].bwd, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
                                 saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
-                                it=self.convs[i].it_bwd)
+                                it=self.convs[i].it_bwd, layout=_lay(sp, i < 3, True))
             C = self.N
         gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad",
-                             prec=self.convs[0].bwd_prec)
+                             prec=self.convs[0].bwd_prec, layout=_lay(sp, True, False))
         return gx
 
 
@@ -77,28 +109,34 @@ class Synthesis:
                                    it_fwd=g6 if i < 6 else 0, it_bwd=g6 if i > 0 else 0)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
+        self.split = _split_capable(self.convs, self.N)
 
-    def forward(self, y4, save=False):
-        h, C, saved = y4, self.M, []
+    def forward(self, y4, save=False, split=None):
+        """split: as Analysis.forward (the inner levels are 2x, 4x, 8x the latent sides: always even)."""
+        sp = self.split if split is None else split
+        h, C, saved = y4, self.M, Saved(split=sp)
         for i in range(3):
             p = self.convs[i]
             h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gdns[i], save,
-                                  tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd)
+                                  tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd,
+                                  layout=_lay(sp, i > 0, True))
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
-        xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS, tag=f"{self.tag}.6.fwd", prec=p.fwd_prec)
+        xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS, tag=f"{self.tag}.6.fwd", prec=p.fwd_prec,
+                             layout=_lay(sp, True, False))
         return xh, saved
 
     def backward(self, gx4, saved):
+        sp = getattr(saved, "split", False)
         g, C = gx4, 3
         for i in (3, 2, 1):
             g, _, _ = K.conv_down(g, C, self.convs[i].bwd, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gdns[i - 1],
                                   saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
-                                  it=self.convs[i].it_bwd)
+                                  it=self.convs[i].it_bwd, layout=_lay(sp, i < 3, True))
             C = self.N
         gy, _, _ = K.conv_down(g, self.N, self.convs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS,
-                               tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec)
+                               tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec, layout=_lay(sp, True, False))
         return gy
 
 

@@ -15,6 +15,8 @@ from ._lib import ConvArgs, call, lib, ptr, stream
 EPI_BIAS, EPI_RELU, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD, EPI_LRELU, EPI_LRELU_BWD = range(8)
 FILL_PLAIN, FILL_LRELU_MASK, FILL_UNSHUFFLE = range(3)
 ORDER_DOWN, ORDER_UP = 0, 1
+# parity-split tensors of an x6 k5 s2 launch (ica_conv_args.layout): the input x, the output-layout tensors
+LAYOUT_IN, LAYOUT_OUT = 1, 2
 GDN_BETA_BOUND = float((1e-6 + 2.0 ** -36) ** 0.5)  # NonNegativeParametrizer bound (utils/ops.py:67)
 
 
@@ -362,15 +364,17 @@ class PackedGDN:
 # Convolutions
 # --------------------------------------------------------------------------- #
 def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False,
-              saved=None, out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
+              saved=None, out=None, tag=None, save_t=None, prec=PREC_FP32, it=0, layout=0):
     """y = conv2d(x, W, stride S, pad KS//2) (+epilogue).  Returns (y4, save_x, save_s).
     save_t: optional nChw4c output of t = dL/dn for the GDN-bwd epilogues (GDN parameter gradients).
     prec=PREC_BF16: bf16-operand launch (wp from pack_conv_bf16; goes through ica_conv_ex).
-    it: the row-tile count wp was packed with (0 = library default; explicit values go through ica_conv_ex)."""
+    it: the row-tile count wp was packed with (0 = library default; explicit values go through ica_conv_ex).
+    layout: parity-split tensors (LAYOUT_IN: x, LAYOUT_OUT: y and the saved / output-layout tensors; x6 only)."""
     N, _, H, W, _ = x4.shape
     tag = _prec_note(tag, prec)
-    if prec in (PREC_BF16, PREC_X6) or it:
-        return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t, prec, it)
+    if prec in (PREC_BF16, PREC_X6) or it or layout:
+        return _conv_prec(x4, Cin, wp, bias, Cout, KS, S, 0, epi, gdn, save, saved, out, tag, save_t, prec, it,
+                          layout)
     Ho = (H + 2 * (KS // 2) - KS) // S + 1
     Wo = (W + 2 * (KS // 2) - KS) // S + 1
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
@@ -391,20 +395,27 @@ def conv_down(x4, Cin, wp, bias, Cout, KS, S, epi=EPI_BIAS, gdn: PackedGDN | Non
 
 
 def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None, save=False, saved=None,
-            out=None, tag=None, save_t=None, prec=PREC_FP32, it=0):
-    """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue)."""
+            out=None, tag=None, save_t=None, prec=PREC_FP32, it=0, layout=0):
+    """y = conv_transpose2d(x, W, stride 2, pad 2, output_padding 1) (+epilogue).  layout: as conv_down (the
+    3-channel output of conv_up3 is always row-major)."""
     N, _, H, W, _ = x4.shape
     tag = _prec_note(tag, prec)
-    if (prec in (PREC_BF16, PREC_X6) or it) and Cout != 3:
-        return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t, prec, it)
+    if (prec in (PREC_BF16, PREC_X6) or it or layout) and Cout != 3:
+        return _conv_prec(x4, Cin, wp, bias, Cout, 5, 2, 1, epi, gdn, save, saved, out, tag, save_t, prec, it,
+                          layout)
     Ho, Wo = 2 * H, 2 * W
     y = out if out is not None else empty_nc4(N, Cout, Ho, Wo, x4.device)
     if Cout == 3:
         if epi != EPI_BIAS:
             raise RuntimeError("conv_up to 3 channels supports the bias epilogue only")
+        if layout & ~LAYOUT_IN or (layout and prec != PREC_X6):
+            raise RuntimeError("conv_up3: parity-split input on the x6 kernel only")
         ev = _ev_begin(tag, N)
-        call({PREC_BF16: "ica_conv_up3_bf16", PREC_X6: "ica_conv_up3_x6"}.get(prec, "ica_conv_up3"), ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
-             Cin, H, W, stream())
+        if prec == PREC_X6:
+            call("ica_conv_up3_x6", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, layout, stream())
+        else:
+            call("ica_conv_up3_bf16" if prec == PREC_BF16 else "ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
+                 Cin, H, W, stream())
         _ev_end(ev)
         return y, None, None
     ss = None
@@ -423,7 +434,7 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     return y, (y if ss is not None else None), ss
 
 
-def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out, tag, save_t, prec, it):
+def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out, tag, save_t, prec, it, layout=0):
     """conv_down / conv_up semantics (returns (y4, save_x, save_s)) through ica_conv_ex: bf16-operand launches and
     explicit row-tile counts."""
     N, _, H, W, _ = x4.shape
@@ -431,13 +442,13 @@ def _conv_prec(x4, Cin, wp, bias, Cout, KS, S, kind, epi, gdn, save, saved, out,
     dt = torch.bfloat16 if prec == PREC_BF16 else torch.float32
     ss = empty_nc4(N, Cout, Ho, Wo, x4.device, dt) if (save and epi in (EPI_GDN, EPI_IGDN)) else None
     y = conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind, epi, it, gdn, save_s=ss, saved=saved, save_t=save_t, out=out,
-                tag=tag, prec=prec)
+                tag=tag, prec=prec, layout=layout)
     return y, (y if ss is not None else None), ss
 
 
 def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: PackedGDN | None = None, res=None,
             save_x=None, save_s=None, saved=None, save_t=None, mask=None, fill_mode=FILL_PLAIN, ps=False,
-            out=None, tag=None, alg_rows=None, prec=PREC_FP32):
+            out=None, tag=None, alg_rows=None, prec=PREC_FP32, layout=0):
     """Generic conv launch (ica_conv_ex).  kind 0: conv2d(x, W, stride S, pad KS//2); kind 1: the stride-2
     transposed conv (dgrad of a stride-2 conv).  fill_mode 2 views x ([N, Cin/16, 2H, 2W, 4]) as the
     PixelUnshuffle(2) tensor [N, Cin/4, H, W, 4] in rho order; ps stores PixelShuffle(2) of the rho-ordered
@@ -474,7 +485,7 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
             gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
     a = ConvArgs(ptr(x4), ptr(y), ptr(wp), ptr(bias), ptr(gp), ptr(None if gdn is None else gdn.beta), ptr(save_x),
                  ptr(save_s), ptr(in_x), ptr(in_s), ptr(save_t), ptr(res), ptr(mask), N, Cin, H, W, Cout, Ho, Wo,
-                 kind, KS, S, epi, it, fill_mode, int(bool(ps)), int(prec))
+                 kind, KS, S, epi, it, fill_mode, int(bool(ps)), int(prec), int(layout))
     import ctypes
     tag = _prec_note(tag, prec)
     ev = _ev_begin(tag, N)

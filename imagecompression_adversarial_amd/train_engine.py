@@ -49,9 +49,15 @@ def gdn_param_grads(raw_beta, raw_gamma, t4, saved, C, g_beta, g_gamma):
     K.reparam_bwd(raw_gamma, dgamma_e, g_gamma, GAMMA_BOUND)
 
 
+def _row_major(saved):
+    if getattr(saved, "split", False):
+        raise RuntimeError("parameter gradients need the forward's activations row-major (forward(..., split=False))")
+
+
 def synthesis_backward(ex, g4, y_in4, saved, params, grads, prefix):
     """g_s backward (engine.Synthesis): the input gradient (returned) and the weight / bias / IGDN parameter
     gradients, written into grads[prefix + name] (CompressAI names: 0.weight, 1.beta, ...)."""
+    _row_major(saved)
     N, M = ex.N, ex.M
     g, C = g4, 3
     for i in (3, 2, 1, 0):
@@ -76,6 +82,7 @@ def synthesis_backward(ex, g4, y_in4, saved, params, grads, prefix):
 def analysis_backward(ex, gy4, x4, saved, params, grads, prefix, input_grad=False):
     """g_a backward (engine.Analysis): weight / bias / GDN parameter gradients into grads[prefix + name], and
     the input gradient (nChw4c, 3 channels) when input_grad."""
+    _row_major(saved)
     N, M = ex.N, ex.M
     g, C = gy4, M
     for i in (3, 2, 1, 0):
@@ -163,7 +170,7 @@ class RDTrainer:
         bscale = 1.0 / (-math.log(2) * npx)
         gscale = bscale * self.lamb_r   # d loss / d log-likelihood (0 in Inf mode)
 
-        y4, sa = ck.ga.forward(x4, save=True)
+        y4, sa = ck.ga.forward(x4, save=True, split=False)   # the wgrad kernels read row-major activations
         yshape = (B, M, H // 16, W // 16)
         if noise_y is None:
             noise_y = torch.empty(yshape, device=x.device).uniform_(-0.5, 0.5)
@@ -185,7 +192,7 @@ class RDTrainer:
             sig4, _, _ = K.conv_down(s2, N, hs.convs[2].fwd, hs.convs[2].bias, M, 3, 1, K.EPI_RELU)
             yt4, ylik4, _ = K.gc_likelihood(y4, M, sig4, None, True, ny4)
             liks = [ylik4, zlik4]
-        xh4, ss = ck.gs.forward(yt4, save=True)
+        xh4, ss = ck.gs.forward(yt4, save=True, split=False)
 
         # ---- loss (train.py:52-96, training=True: no clamp on x_hat) ----
         bpp = sum(torch.log(l.clamp_min(1.0 / 65536)).sum() for l in liks) * bscale

@@ -84,10 +84,11 @@ size_t ica_pack_gdn_x6_size(int C);
 size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it);
 /* bf16 Z-gather transposed conv to 3 channels (g_s last layer / g_a first-layer input-gradient). */
 /* fp32-accurate bf16x6 conv_up3 (prec 2): three bf16 planes of the ica_pack_up3 fragment order
- * (3 * ica_pack_up3_size(Cin) values); same semantics and argument meaning as ica_conv_up3. */
+ * (3 * ica_pack_up3_size(Cin) values); same semantics and argument meaning as ica_conv_up3.  layout: 1 = x is
+ * parity-split (ica_conv_args.layout; Cin 128 / 192, even Hin / Win), 0 = row-major. */
 int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t stream);
 int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
-                    hipStream_t stream);
+                    int layout, hipStream_t stream);
 int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t stream);
 int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
                       hipStream_t stream);
@@ -183,6 +184,10 @@ typedef struct ica_conv_args {
              * 2: fp32-accurate bf16x6 operands (wp from ica_pack_conv_weight_x6, gp from ica_pack_gdn_x6, fp32
              * x / y / saved tensors; k5 s2, Cin >= 16: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD, 128 output channels,
              * or 96-multiples with the bias epilogue) */
+  int layout; /* parity-split pixel order (prec 2, k5 s2 only; 0 = row-major everywhere): bit 0 = x, bit 1 = y and
+               * every other output-layout tensor (save_x / save_s, in_x / in_s, save_t, res).  A parity-split
+               * H x W plane (H, W even) stores the four (y & 1, x & 1) sub-planes of (H/2) x (W/2) pixels one after
+               * another, so a transposed conv's output-parity classes write and read dense lines */
 } ica_conv_args;
 int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);
 /* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
