@@ -56,27 +56,42 @@ TAGS = {   # epilogue ids: 0 BIAS, 2 GDN, 3 IGDN, 4 GDN_BWD, 5 IGDN_BWD
     "g_a.0.dgrad": up3(*h[1]),
 }
 
-if PREC == "x6":   # ica_conv_x6.hip launchers (and the x6 Z-gather)
+if PREC == "x6":   # ica_conv_x6.hip launchers (and the x6 conv_up3); names carry the PT template argument
     NS = "void (anonymous namespace)::"
 
     def down_x6(epi, Hout, Wout, Cout, it):
-        return f"{NS}conv_down_x6_kernel<{it}, {epi}>", -(-Wout // 32) * -(-Hout // 8) * B * 256 * -(-Cout // (it * 32))
+        ncb = -(-Cout // (it * 32))
+        b2 = -(-Wout // 32) * -(-Hout // 8) * B * ncb
+        pt = 2 if b2 >= 256 else 1
+        return f"{NS}conv_down_x6_kernel<{it}, {epi}, {pt}>", -(-Wout // 32) * -(-Hout // (4 * pt)) * B * 256 * ncb
 
     def rgb_x6(epi, Hout, Wout, Cout):
-        return f"{NS}conv_rgb_x6_kernel<4, {epi}>", -(-Wout // 32) * -(-Hout // 4) * B * 256 * -(-Cout // 128)
+        tiles = -(-Wout // 32) * -(-Hout // 4) * B
+        if epi in (4, 5):   # persistent GDN-backward form: one block per CU, contiguous tile runs
+            per = -(-tiles // min(tiles, 256))
+            return f"{NS}conv_rgb_bwd_x6_kernel<4, {epi}>", -(-tiles // per) * 256
+        return f"{NS}conv_rgb_x6_kernel<4, {epi}>", tiles * 256 * -(-Cout // 128)
 
     def up_x6(epi, Hin, Win, Cin, Cout):
         cg = 128 if Cin <= 128 else 64
-        return f"{NS}conv_up_x6_kernel<4, {epi}, {cg}>", -(-Win // 16) * -(-Hin // 8) * B * 256 * -(-Cout // 128)
+        ncb = -(-Cout // 128)
+        fill = lambda n: n / (-(-n // 256) * 256)   # noqa: E731  (launch_up_x6's round fill)
+        b2 = -(-Win // 16) * -(-Hin // 8) * B * ncb
+        b1 = -(-Win // 16) * -(-Hin // 4) * B * ncb
+        pt = 1 if fill(b1) > fill(b2) + 0.15 else 2
+        return f"{NS}conv_up_x6_kernel<4, {epi}, {cg}, {pt}>", (b1 if pt == 1 else b2) * 256
 
     def up3_x6(Hin, Win):
-        return "void conv_up3_kernel<false, true>", -(-Win // 32) * -(-Hin // 5) * B * 256
+        ct = 3   # Cin = 128: 10 x 30 input tiles, persistent
+        tiles = -(-Win // 30) * -(-Hin // (4 * ct - 2)) * B
+        per = -(-tiles // min(tiles, 256))
+        return "void conv_up3_x6p_kernel<8, 3>", -(-tiles // per) * 256
 
     TAGS = {
         "g_a.0.fwd": rgb_x6(2, *h[1], N), "g_a.2.fwd": down_x6(2, *h[2], N, 4),
         "g_a.4.fwd": down_x6(2, *h[3], N, 4), "g_a.6.fwd": down_x6(0, *h[4], M, 3),
         "g_s.0.fwd": up_x6(3, *h[4], M, N), "g_s.2.fwd": up_x6(3, *h[3], N, N), "g_s.4.fwd": up_x6(3, *h[2], N, N),
-        "g_s.6.fwd": up3_x6(*h[1]),
+        "g_s.6.fwd": up3_x6(*h[1]),    # shares its name and grid with g_a.0.dgrad
         "g_s.6.dgrad": rgb_x6(5, *h[1], N), "g_s.4.dgrad": down_x6(5, *h[2], N, 4),
         "g_s.2.dgrad": down_x6(5, *h[3], N, 4), "g_s.0.dgrad": down_x6(0, *h[4], M, 3),
         "g_a.6.dgrad": up_x6(4, *h[4], M, N), "g_a.4.dgrad": up_x6(4, *h[3], N, N), "g_a.2.dgrad": up_x6(4, *h[2], N, N),
