@@ -1275,25 +1275,40 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int 
     b0 = tx * U3_OW;
     n = r / tiles_y;
   };
-  // activations of (column tile ct, chunk ch): channels 16 ch + 8 h .. + 7 of halo pixel (row wave + 4 ct, col j);
-  // pixels outside the image read past the descriptor's range (zeros)
-  f32x4 xa[CT][NCH][2];
-  auto load_chunk = [&](int t, int ct, int ch) __attribute__((always_inline)) {
+  // activations of (column tile ct, chunk ch): channels 16 ch + 8 h .. + 7 of halo pixel (row wave + 4 ct, col j).
+  // Per tile, once: the image's descriptor and, per column tile, the byte offset of the lane's first quad (chunk 0,
+  // quad 2h), or OOB for pixels outside the image and for the "next tile" past the block's run (the loads then
+  // return zeros: no branches in the MFMA loop)
+  const bool split_in = (p.pl & PL_IN) != 0;
+  const unsigned qs = plane * 16u, cs = 4u * qs;   // second quad, next chunk (bytes)
+  constexpr unsigned OOB = 0xFFFFFFF0u;
+  auto prep = [&](int t, bool real, __amdgpu_buffer_rsrc_t& r, unsigned (&vb)[CT]) __attribute__((always_inline)) {
     int n, a0, b0;
-    coords(t, n, a0, b0);
-    const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
-    const int iy = a0 - 1 + wave + 4 * ct, ix = b0 - 1 + j;
-    const bool ok = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const unsigned o0 =
-        ok ? ((unsigned)(4 * ch + 2 * h) * plane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u : 0xFFFFFFF0u;
-    xa[ct][ch][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o0, 0, 0));
-    xa[ct][ch][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? o0 + plane * 16u : 0xFFFFFFF0u,
-                                                                                     0, 0));
+    coords(real ? t : t_begin, n, a0, b0);
+    r = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
+    const int ix = b0 - 1 + j;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int iy = a0 - 1 + wave + 4 * ct;
+      const bool ok = real && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      vb[ct] = ok ? ((unsigned)(2 * h) * plane + pix_at(iy, ix, p.Hin, p.Win, split_in)) * 16u : OOB;
+    }
   };
+  f32x4 xa[CT][NCH][2];
+  auto load = [&](const __amdgpu_buffer_rsrc_t& r, const unsigned (&vb)[CT], int ct, int ch)
+      __attribute__((always_inline)) {
+    const bool ok = vb[ct] != OOB;
+    const unsigned o = vb[ct] + (unsigned)ch * cs;
+    xa[ct][ch][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? o : OOB, 0, 0));
+    xa[ct][ch][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? o + qs : OOB, 0, 0));
+  };
+  __amdgpu_buffer_rsrc_t rn;
+  unsigned vbn[CT];
+  prep(t_begin, true, rn, vbn);
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) load_chunk(t_begin, ct, ch);
+    for (int ch = 0; ch < NCH; ++ch) load(rn, vbn, ct, ch);
   constexpr long pst = 3L * NCH * 64;   // fragments per plane
   const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * pst * 16));
   int wz = 0;   // a per-tile "zero" (keeps the fragment offsets from being hoisted into SGPRs across the tile loop)
@@ -1303,12 +1318,17 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int 
 #pragma unroll
       for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, wz + (int)((q * pst + ((long)it * NCH + ch) * 64) * 16));
   };
+  auto split = [&](int ct, int ch, bf16x8 (&b)[3]) __attribute__((always_inline)) {
+    const float v[8] = {xa[ct][ch][0][0], xa[ct][ch][0][1], xa[ct][ch][0][2], xa[ct][ch][0][3],
+                        xa[ct][ch][1][0], xa[ct][ch][1][1], xa[ct][ch][1][2], xa[ct][ch][1][3]};
+    split3x8(v, b);
+  };
   const float bias0 = p.bias ? p.bias[0] : 0.f, bias1 = p.bias ? p.bias[1] : 0.f, bias2 = p.bias ? p.bias[2] : 0.f;
 #pragma unroll 1
   for (int t = t_begin; t < t_end; ++t) {
     wz = 0;
     asm volatile("" : "+s"(wz));
-    const bool more = t + 1 < t_end;
+    prep(t + 1, t + 1 < t_end, rn, vbn);
     f32x16 acc[CT][3];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
@@ -1316,19 +1336,33 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int 
       for (int it = 0; it < 3; ++it) acc[ct][it] = f32x16{0};
     bf16x8 wa[2][3][3];
     ldw(wa[0], 0);
+    // software pipeline: the B operand of step (ct, ch) is split during the MFMAs of the step before (interleaved
+    // 3 VALU per MFMA); the step's registers then take tile t+1's chunk
+    bf16x8 bc[3];
+    split(0, 0, bc);
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
       if (ch + 1 < NCH) ldw(wa[(ch + 1) & 1], ch + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        const float v[8] = {xa[ct][ch][0][0], xa[ct][ch][0][1], xa[ct][ch][0][2], xa[ct][ch][0][3],
-                            xa[ct][ch][1][0], xa[ct][ch][1][1], xa[ct][ch][1][2], xa[ct][ch][1][3]};
-        bf16x8 b[3];
-        split3x8(v, b);
+        const int nct = ct + 1 < CT ? ct + 1 : 0, nch = ct + 1 < CT ? ch : ch + 1;
+        bf16x8 bn[3];
+        if (nch < NCH) split(nct, nch, bn);
 #pragma unroll
-        for (int it = 0; it < 3; ++it) acc[ct][it] = mfma_x6(wa[ch & 1][it], b, acc[ct][it]);
-        if (more) load_chunk(t + 1, ct, ch);   // the registers just consumed take tile t+1's chunk
+        for (int it = 0; it < 3; ++it) acc[ct][it] = mfma_x6(wa[ch & 1][it], bc, acc[ct][it]);
+        load(rn, vbn, ct, ch);   // the registers just consumed take tile t+1's chunk
+#pragma unroll
+        for (int k = 0; k < 18; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // up to three VALU (the next operand's split)
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // the two activation loads
+        __builtin_amdgcn_sched_barrier(0);
+        if (nch < NCH) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bc[q] = bn[q];
+        }
       }
     }
     __syncthreads();   // the previous tile's gather is done with zs
@@ -1348,6 +1382,7 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int 
     // one 32-B run
     int n, a0, b0;
     coords(t, n, a0, b0);
+#pragma unroll 1
     for (int idx = threadIdx.x; idx < R * U3_OW; idx += 256) {
       const int al = idx / U3_OW, bl = idx - al * U3_OW;
       const int a = a0 + al, b = b0 + bl;
