@@ -36,13 +36,13 @@ _SIGS = {
     "ica_pack_up3_bf16": [_p, _p, _i, _p],
     "ica_pack_up3_x6": [_p, _p, _i, _p],
     "ica_conv_up3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
-    "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_gdn_bf16": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_up3_size": [_i],
     "ica_pack_up3": [_p, _p, _i, _p],
-    "ica_conv_up3": [_p, _p, _p, _p, _i, _i, _i, _i, _p],
+    "ica_conv_up3": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_down": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "ica_conv_up": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
     "ica_elem_blocks_per_image": [],

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
         v = ld4(p.x + ((((size_t)n * (Cin4 >> 2) + c4g) * (2 * p.Hin) + 2 * iy + (q >> 1)) * (2 * p.Win) +
                        2 * ix + (q & 1)) * 4);
       } else {
-        const size_t xo = ((((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix) * 4;
+        const size_t xo = (((size_t)n * Cin4 + c4) * ((size_t)p.Hin * p.Win) + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 4;
         v = ld4(p.x + xo);
         if constexpr ((FX & FX_MASK) != 0) {
           const f32x4 m = ld4(p.mask + xo);
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
           const int c4 = ch * NQ + 2 * q;
           const bool ok = i0 + i < NF && e < NE * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 &&
                           ix < p.Win;
-          const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 8u;
+          const unsigned vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 8u;
           va[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
           vb[i] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo + xplane * 8u : 0xFFFFFFF0u,
                                                                                  0, 0));
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
             const int c4g = c4 >> 2, sq = c4 & 3;
             vo = (((unsigned)c4g * (2 * p.Hin) + 2 * iy + (sq >> 1)) * (2 * p.Win) + 2 * ix + (sq & 1)) * 16u;
           } else {
-            vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+            vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
           }
           v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
           if constexpr (MK)
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
         const int iy = iy0 + pr, ix = ix0 + pc;
         const int c4 = ch * NQ + q;
         const bool ok = e < NE * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-        const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+        const unsigned vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
         v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
       }
       __syncthreads();
@@ -309,7 +309,8 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
         const int c4 = ch * NQ + 2 * q;
         u32x2 a = {0u, 0u}, b = {0u, 0u};
         if (c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
-          const u32x2* xb = reinterpret_cast<const u32x2*>(p.x) + (((size_t)n * Cin4 + c4) * p.Hin + iy) * p.Win + ix;
+          const u32x2* xb =
+              reinterpret_cast<const u32x2*>(p.x) + ((size_t)n * Cin4 + c4) * ((size_t)p.Hin * p.Win) + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN);
           a = xb[0];
           b = xb[(size_t)p.Hin * p.Win];
         }
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void conv_down_split_kernel(ConvParams p) {
       const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
       const int iy = iy0 + pr, ix = ix0 + pc, c4 = ch * NQ + q;
       const bool ok = e < NQ * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const unsigned vo = ((unsigned)c4 * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      const unsigned vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
       v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
     }
     __syncthreads();
@@ -864,7 +865,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
       const int q = e / UP_PLANE, rem = e - q * UP_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
       const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
       const bool ok = e < total && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const unsigned vo = ((unsigned)(BF ? 2 * q : q) * xplane + (unsigned)iy * p.Win + ix) * qbytes;
+      const unsigned vo = ((unsigned)(BF ? 2 * q : q) * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * qbytes;
       if constexpr (BF) {  // bf16 activations: two 8-B channel quads per 16-B LDS entry
         const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
         const u32x2 hi = __builtin_bit_cast(
@@ -930,7 +931,7 @@ __global__ __launch_bounds__(256, 2) void conv_up_small_kernel(ConvParams p) {
       const int q = e / UPS_PLANE, rem = e - q * UPS_PLANE, pr = rem / UP_PC, pc = rem - pr * UP_PC;
       const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
       const bool ok = e < total && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const unsigned vo = ((unsigned)q * xplane + (unsigned)iy * p.Win + ix) * 16u;
+      const unsigned vo = ((unsigned)q * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
       v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
     }
 #pragma unroll
@@ -1043,7 +1044,7 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
         const int hr = q / T3_HC, hc = q - hr * T3_HC;
         const int iy = a0 - 1 + hr, ix = b0 - 1 + hc;
         const bool ok = wave + 4 * k < T3_JT && q < T3_NPX && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-        const unsigned po = (unsigned)(iy * p.Win + ix) * 8u;
+        const unsigned po = pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN) * 8u;
 #pragma unroll
         for (int ch = 0; ch < T3_NCH_BF; ++ch)
 #pragma unroll
@@ -1085,7 +1086,8 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
     const int hr = q / T3_HC, hc = q - hr * T3_HC;
     const int iy = a0 - 1 + hr, ix = b0 - 1 + hc;
     const bool ok = q < T3_NPX && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const float* xp = p.x + (((size_t)n * Cin4) * plane + (ok ? (size_t)iy * p.Win + ix : 0)) * 4;
+    const size_t pix = ok ? (size_t)pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN) : 0;
+    const float* xp = p.x + (((size_t)n * Cin4) * plane + pix) * 4;
     f32x16 acc[3];
 #pragma unroll
     for (int it = 0; it < 3; ++it) acc[it] = f32x16{0};
@@ -1093,7 +1095,7 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
       // bf16: the 8 channels a lane loads are the k = 8h..8h+7 slice of ONE 32x32x16 MFMA per tile, so a
       // chunk is 3 MFMAs; the B loads (HBM) and A loads (L2) of 4 chunks are issued before their MFMAs.
       const bf16x8* wl = reinterpret_cast<const bf16x8*>(p.wp) + lane;
-      const u32x2* xq = reinterpret_cast<const u32x2*>(p.x) + (((size_t)n * Cin4) * plane + (ok ? (size_t)iy * p.Win + ix : 0));
+      const u32x2* xq = reinterpret_cast<const u32x2*>(p.x) + (((size_t)n * Cin4) * plane + pix);
 #pragma unroll 1
       for (int ch0 = 0; ch0 < nch; ch0 += 4) {
         f32x4 v0[4];
@@ -1123,7 +1125,7 @@ __global__ __launch_bounds__(256, T3_BLOCKS) void conv_up3_kernel(ConvParams p) 
       const long pst = 3L * nch * 64;   // fragments per plane
       const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * pst * 16));
       const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
-      const unsigned po = ok ? (unsigned)(iy * p.Win + ix) * 16u : 0xFFFFFFF0u;
+      const unsigned po = ok ? (unsigned)pix * 16u : 0xFFFFFFF0u;
       auto load = [&](int ch, bf16x8 (&a)[3][3], f32x4& v0, f32x4& v1) {
 #pragma unroll
         for (int it = 0; it < 3; ++it)
@@ -1966,11 +1968,20 @@ int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t st) {
   return 0;
 }
 
+// layout: PL_IN = x parity-split (the 3-channel output, the image, is always row-major)
+static int up3_layout_ok(int layout, int Hin, int Win) {
+  if (layout & ~PL_IN) return -4;
+  if ((layout & PL_IN) && ((Hin | Win) & 1)) return -2;
+  return 0;
+}
+
 int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
-                 hipStream_t st) {
+                 int layout, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
+  if (const int rc = up3_layout_ok(layout, Hin, Win)) return rc;
   ConvParams p{x, y, wp, bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, Cin, Hin, Win, 3,
                2 * Hin, 2 * Win, nullptr};
+  p.pl = layout;
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
   hipLaunchKernelGGL(conv_up3_kernel<false>, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
@@ -1991,8 +2002,7 @@ int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t st) {
 int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
                     int layout, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
-  if (layout & ~PL_IN) return -4;   // the 3-channel output is the image: row-major
-  if ((layout & PL_IN) && ((Hin | Win) & 1 || (Cin != 128 && Cin != 192))) return -2;
+  if (const int rc = up3_layout_ok(layout, Hin, Win)) return rc;
   ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
   p.pl = layout;
@@ -2025,10 +2035,12 @@ int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t st) {
 }
 
 int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
-                      hipStream_t st) {
+                      int layout, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
+  if (const int rc = up3_layout_ok(layout, Hin, Win)) return rc;
   ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
+  p.pl = layout;
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
   hipLaunchKernelGGL(conv_up3_kernel<true>, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
@@ -2116,9 +2128,9 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
                a->N,    a->Cin,  a->Hin,  a->Win,  a->Cout, a->Hout, a->Wout,   a->save_t, a->res,  a->mask,
                a->fill_mode, a->ps, a->prec, a->layout};
   if (a->prec != 0 && a->prec != 1 && a->prec != 2) return -4;
-  // parity-split tensors: x6 k5 s2 launches only (ica_conv_x6_dispatch checks the rest), even planes
+  // parity-split tensors: the k5 s2 layers of the bmshj2018 transforms (plain fill, no PixelShuffle), even planes
   if (a->layout & ~(PL_IN | PL_OUT)) return -4;
-  if (a->layout && (a->prec != 2 || a->KS != 5 || a->S != 2)) return -4;
+  if (a->layout && (a->KS != 5 || a->S != 2 || a->fill_mode != 0 || a->ps)) return -4;
   if (((a->layout & PL_IN) && ((a->Hin | a->Win) & 1)) || ((a->layout & PL_OUT) && ((a->Hout | a->Wout) & 1)))
     return -2;
   const int it = resolve_it(a->Cout, a->it);

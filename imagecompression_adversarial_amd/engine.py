@@ -26,23 +26,49 @@ def _P(sd, prefix, name):
 
 
 class Saved(list):
-    """The per-layer (y, s) pairs a forward saves for its backward, and whether the inner levels were stored
-    parity-split (the backward must address them the same way)."""
+    """The per-layer (y, s) pairs a forward saves for its backward, and which levels (L0 = image ... L4 = latent)
+    were stored parity-split (the backward must address them the same way)."""
 
-    def __init__(self, items=(), split=False, exact=True):
+    def __init__(self, items=(), split=(False,) * 5, exact=True):
         super().__init__(items)
-        self.split = split
+        self.split = tuple(split)
         self.exact = exact   # every level exactly halves the one above (input sides multiples of 16)
 
 
-def _lay(split, inp, out):
-    return (K.LAYOUT_IN if split and inp else 0) | (K.LAYOUT_OUT if split and out else 0)
+def _layout_of(saved):
+    """The forward's layout record; a plain list would lose it (and a split forward would be misread)."""
+    if not isinstance(saved, Saved):
+        raise TypeError("backward needs the forward's Saved record (keep its type when selecting rows)")
+    return saved.split
 
 
-def _split_capable(convs, N):
-    """Parity-split inner levels (L1-L3 of the k5 s2 stacks): every launch touching them runs an x6 kernel (the
-    only kernels that address that order), the 3-channel end on the x6 conv_up3 (N = 128 / 192)."""
-    return N in (128, 192) and all(c.fwd_prec == K.PREC_X6 and c.bwd_prec == K.PREC_X6 for c in convs)
+def _lay(lv, a, b):
+    """layout of a launch from level a to level b"""
+    return (K.LAYOUT_IN if lv[a] else 0) | (K.LAYOUT_OUT if lv[b] else 0)
+
+
+def _levels(split):
+    """split (True / False / per-level (L1, L2, L3) flags) -> flags of L0..L4 (the image and the latent: never)"""
+    if isinstance(split, (tuple, list)):
+        s = tuple(bool(v) for v in split)
+    else:
+        s = (bool(split),) * 3
+    return (False,) + s + (False,)
+
+
+def _split_policy(convs):
+    """Which inner levels (L1, L2, L3) of the k5 s2 stacks are stored parity-split (§3e).  Every conv kernel
+    addresses that order (ica_conv_args.layout), so this is a measured choice per operand path (config-2 / config-5
+    shapes): x6 gains on every level (the conv_up stores and GDN-backward reads are dense, and the x6 conv_up3 and
+    RGB-end kernels are indifferent); bf16 gains on L2 / L3 but its RGB-end kernels (the RGB GDN forward store,
+    the Z-gather loads) lose more than the L1 conv_up launches gain; the fp32 kernels are MFMA-bound, the split's
+    address arithmetic costs ~1 %."""
+    precs = {c.fwd_prec for c in convs} | {c.bwd_prec for c in convs}
+    if precs == {K.PREC_X6}:
+        return (True, True, True)
+    if K.PREC_BF16 in precs:
+        return (False, True, True)
+    return (False, False, False)
 
 
 class Analysis:
@@ -58,41 +84,43 @@ class Analysis:
                                    it_fwd=g6 if i < 6 else 0, it_bwd=g6 if i > 0 else 0)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
-        self.split = _split_capable(self.convs, self.N)
+        self.split = _split_policy(self.convs)
 
     def forward(self, x4, save=False, split=None):
-        """split: store the inner levels L1-L3 parity-split (default: when every launch runs x6 and every inner
-        level has even sides; the transform's output y and its input gradient stay row-major either way)."""
+        """split: which inner levels (L1, L2, L3) to store parity-split (True / False / per-level flags; default
+        the operand path's policy), each only when its sides are even; the transform's output y and its input
+        gradient stay row-major either way."""
         H, W = x4.shape[2], x4.shape[3]
-        sides = [((H + (1 << k) - 1) >> k, (W + (1 << k) - 1) >> k) for k in (1, 2, 3)]
-        sp = (self.split if split is None else split) and all(a % 2 == 0 and b % 2 == 0 for a, b in sides)
-        h, C, saved = x4, 3, Saved(split=sp, exact=H % 16 == 0 and W % 16 == 0)
-        for i in range(3):
+        lv = _levels(self.split if split is None else split)
+        lv = tuple(f and ((H + (1 << k) - 1) >> k) % 2 == 0 and ((W + (1 << k) - 1) >> k) % 2 == 0
+                   for k, f in enumerate(lv))
+        h, C, saved = x4, 3, Saved(split=lv, exact=H % 16 == 0 and W % 16 == 0)
+        for i in range(3):   # layer i: level i -> level i + 1
             p = self.convs[i]
             h, sx, ss = K.conv_down(h, C, p.fwd, p.bias, self.N, 5, 2, K.EPI_GDN, self.gdns[i], save,
                                     tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd,
-                                    layout=_lay(sp, i > 0, True))
+                                    layout=_lay(lv, i, i + 1))
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
         y, _, _ = K.conv_down(h, self.N, p.fwd, p.bias, self.M, 5, 2, K.EPI_BIAS, tag=f"{self.tag}.6.fwd",
-                              prec=p.fwd_prec, layout=_lay(sp, True, False))
+                              prec=p.fwd_prec, layout=_lay(lv, 3, 4))
         return y, saved
 
     def backward(self, gy4, saved):
-        if not getattr(saved, "exact", True):
+        lv = _layout_of(saved)
+        if not saved.exact:
             # the input gradients are 2x transposed convs: an odd level (sides not multiples of 16) has no
             # exact transpose here (the attack pads its images to multiples of 64, coder.read_image)
             raise ValueError("g_a input gradient: image sides must be multiples of 16")
-        sp = getattr(saved, "split", False)
         g, C = gy4, self.M
         for i in (3, 2, 1):
             g, _, _ = K.conv_up(g, C, self.convs[i].bwd, None, self.N, K.EPI_GDN_BWD, self.gdns[i - 1],
                                 saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
-                                it=self.convs[i].it_bwd, layout=_lay(sp, i < 3, True))
+                                it=self.convs[i].it_bwd, layout=_lay(lv, i + 1, i))
             C = self.N
         gx, _, _ = K.conv_up(g, self.N, self.convs[0].bwd, None, 3, K.EPI_BIAS, tag=f"{self.tag}.0.dgrad",
-                             prec=self.convs[0].bwd_prec, layout=_lay(sp, True, False))
+                             prec=self.convs[0].bwd_prec, layout=_lay(lv, 1, 0))
         return gx
 
 
@@ -109,34 +137,34 @@ class Synthesis:
                                    it_fwd=g6 if i < 6 else 0, it_bwd=g6 if i > 0 else 0)
                       for i in (0, 2, 4, 6)]
         self.gdns = [K.PackedGDN(_P(sd, prefix, f"{i}.beta"), _P(sd, prefix, f"{i}.gamma")) for i in (1, 3, 5)]
-        self.split = _split_capable(self.convs, self.N)
+        self.split = _split_policy(self.convs)
 
     def forward(self, y4, save=False, split=None):
         """split: as Analysis.forward (the inner levels are 2x, 4x, 8x the latent sides: always even)."""
-        sp = self.split if split is None else split
-        h, C, saved = y4, self.M, Saved(split=sp)
-        for i in range(3):
+        lv = _levels(self.split if split is None else split)
+        h, C, saved = y4, self.M, Saved(split=lv)
+        for i in range(3):   # layer i: level 4 - i -> level 3 - i
             p = self.convs[i]
             h, sx, ss = K.conv_up(h, C, p.fwd, p.bias, self.N, K.EPI_IGDN, self.gdns[i], save,
                                   tag=f"{self.tag}.{2 * i}.fwd", prec=p.fwd_prec, it=p.it_fwd,
-                                  layout=_lay(sp, i > 0, True))
+                                  layout=_lay(lv, 4 - i, 3 - i))
             saved.append((sx, ss))
             C = self.N
         p = self.convs[3]
         xh, _, _ = K.conv_up(h, self.N, p.fwd, p.bias, 3, K.EPI_BIAS, tag=f"{self.tag}.6.fwd", prec=p.fwd_prec,
-                             layout=_lay(sp, True, False))
+                             layout=_lay(lv, 1, 0))
         return xh, saved
 
     def backward(self, gx4, saved):
-        sp = getattr(saved, "split", False)
+        lv = _layout_of(saved)
         g, C = gx4, 3
-        for i in (3, 2, 1):
+        for i in (3, 2, 1):   # level 3 - i -> level 4 - i
             g, _, _ = K.conv_down(g, C, self.convs[i].bwd, None, self.N, 5, 2, K.EPI_IGDN_BWD, self.gdns[i - 1],
                                   saved=saved[i - 1], tag=f"{self.tag}.{2 * i}.dgrad", prec=self.convs[i].bwd_prec,
-                                  it=self.convs[i].it_bwd, layout=_lay(sp, i < 3, True))
+                                  it=self.convs[i].it_bwd, layout=_lay(lv, 3 - i, 4 - i))
             C = self.N
         gy, _, _ = K.conv_down(g, self.N, self.convs[0].bwd, None, self.M, 5, 2, K.EPI_BIAS,
-                               tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec, layout=_lay(sp, True, False))
+                               tag=f"{self.tag}.0.dgrad", prec=self.convs[0].bwd_prec, layout=_lay(lv, 3, 4))
         return gy
 
 

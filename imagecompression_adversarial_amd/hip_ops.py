@@ -408,14 +408,9 @@ def conv_up(x4, Cin, wp, bias, Cout, epi=EPI_BIAS, gdn: PackedGDN | None = None,
     if Cout == 3:
         if epi != EPI_BIAS:
             raise RuntimeError("conv_up to 3 channels supports the bias epilogue only")
-        if layout & ~LAYOUT_IN or (layout and prec != PREC_X6):
-            raise RuntimeError("conv_up3: parity-split input on the x6 kernel only")
         ev = _ev_begin(tag, N)
-        if prec == PREC_X6:
-            call("ica_conv_up3_x6", ptr(x4), ptr(y), ptr(wp), ptr(bias), N, Cin, H, W, layout, stream())
-        else:
-            call("ica_conv_up3_bf16" if prec == PREC_BF16 else "ica_conv_up3", ptr(x4), ptr(y), ptr(wp), ptr(bias), N,
-                 Cin, H, W, stream())
+        call({PREC_BF16: "ica_conv_up3_bf16", PREC_X6: "ica_conv_up3_x6"}.get(prec, "ica_conv_up3"), ptr(x4), ptr(y),
+             ptr(wp), ptr(bias), N, Cin, H, W, int(layout), stream())
         _ev_end(ev)
         return y, None, None
     ss = None

@@ -329,7 +329,10 @@ def _select(saved, rows):
         return None
     if isinstance(saved, torch.Tensor):
         return saved.index_select(0, rows)
-    return type(saved)(_select(s, rows) for s in saved)
+    out = type(saved)(_select(s, rows) for s in saved)
+    if hasattr(saved, "__dict__"):   # engine.Saved: keep the layout record (split / exact) of the selection
+        out.__dict__.update(saved.__dict__)
+    return out
 
 
 class DefendedAttackLoop(AttackLoop):

@@ -91,7 +91,7 @@ int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias,
                     int layout, hipStream_t stream);
 int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t stream);
 int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
-                      hipStream_t stream);
+                      int layout, hipStream_t stream);
 /* bf16 conv path activations are bf16 nChw4c (8 B per channel quad): every prec = 1 conv_down / conv_up reads
  * bf16 x (except 4-channel RGB inputs, fp32), writes bf16 y / save_s and reads bf16 in_x / in_s; the Z-gather
  * kernel reads bf16 x and writes fp32 y.  Casts for the tensors that leave the path (n % 4 == 0): */
@@ -184,17 +184,18 @@ typedef struct ica_conv_args {
              * 2: fp32-accurate bf16x6 operands (wp from ica_pack_conv_weight_x6, gp from ica_pack_gdn_x6, fp32
              * x / y / saved tensors; k5 s2, Cin >= 16: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD, 128 output channels,
              * or 96-multiples with the bias epilogue) */
-  int layout; /* parity-split pixel order (prec 2, k5 s2 only; 0 = row-major everywhere): bit 0 = x, bit 1 = y and
+  int layout; /* parity-split pixel order (k5 s2, plain fill, no ps; 0 = row-major everywhere): bit 0 = x, bit 1 = y and
                * every other output-layout tensor (save_x / save_s, in_x / in_s, save_t, res).  A parity-split
                * H x W plane (H, W even) stores the four (y & 1, x & 1) sub-planes of (H/2) x (W/2) pixels one after
                * another, so a transposed conv's output-parity classes write and read dense lines */
 } ica_conv_args;
 int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);
-/* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5]. */
+/* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5].  layout: 1 = x parity-split
+ * (ica_conv_args.layout bit 0; even Hin / Win), 0 = row-major; the 3-channel output is always row-major. */
 size_t ica_pack_up3_size(int Cin);
 int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t stream);
 int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, int N, int Cin, int Hin, int Win,
-                 hipStream_t stream);
+                 int layout, hipStream_t stream);
 
 /* ---- elementwise / attack step / entropy (ica_elem.hip) -------------------- */
 int ica_elem_blocks_per_image(void);

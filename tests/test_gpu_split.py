@@ -143,35 +143,40 @@ def test_rgb_ends_split(B, H, W):
         _same(o1, o0)
 
 
-def test_split_rejected_off_x6():
-    """Only the x6 k5 s2 launches address the split order: fp32 / bf16 launches and odd planes are refused."""
+def test_split_rejected_outside_k5s2():
+    """The split order is addressed by the k5 s2 launches (plain fill, no PixelShuffle) and needs even planes: a
+    k3 s1 launch (cheng2020's convs) and an odd plane are refused, not silently misread."""
     from imagecompression_adversarial_amd import hip_ops as K
-    gd, _, _, _, _ = _layers()
     g = _gen(13)
-    w = (torch.rand(128, 128, 5, 5, generator=g, device=DEV) - 0.5) * 0.04
-    p32 = K.PackedConv(w, None, "conv", 2, K.PREC_FP32)
+    w3 = (torch.rand(128, 128, 3, 3, generator=g, device=DEV) - 0.5) * 0.04
+    p3 = K.PackedConv(w3, None, "conv", 1, K.PREC_FP32)
     x = _act(1, 128, 32, 32, 14)
     with pytest.raises(RuntimeError):
-        K.conv_down(x, 128, p32.fwd, None, 128, 5, 2, K.EPI_BIAS, layout=K.LAYOUT_IN)
-    px6 = K.PackedConv(w, None, "conv", 2, K.PREC_X6)
-    with pytest.raises(RuntimeError):   # 17 x 17 output: an odd plane cannot be split
-        K.conv_down(_act(1, 128, 34, 34, 15), 128, px6.fwd, None, 128, 5, 2, K.EPI_BIAS, prec=K.PREC_X6,
-                    layout=K.LAYOUT_OUT)
+        K.conv_ex(x, 128, p3.fwd, None, 128, 3, 1, 0, K.EPI_BIAS, layout=K.LAYOUT_IN)
+    w5 = (torch.rand(128, 128, 5, 5, generator=g, device=DEV) - 0.5) * 0.04
+    for prec in (K.PREC_FP32, K.PREC_X6):
+        p5 = K.PackedConv(w5, None, "conv", 2, prec)
+        with pytest.raises(RuntimeError):   # 17 x 17 output: an odd plane cannot be split
+            K.conv_down(_act(1, 128, 34, 34, 15), 128, p5.fwd, None, 128, 5, 2, K.EPI_BIAS, prec=p5.fwd_prec,
+                        layout=K.LAYOUT_OUT)
 
 
-def _kern(P):
+def _kern(P, precision="x6"):
     from imagecompression_adversarial_amd.engine import CodecKernels
-    return CodecKernels({k: v.to(DEV) for k, v in P.items()}, "hyper", precision="x6")
+    return CodecKernels({k: v.to(DEV) for k, v in P.items()}, "hyper", precision=precision)
 
 
-@pytest.mark.parametrize("H,W,expect_split", [(128, 192, True), (64, 96, True), (136, 200, False)])
-def test_chain_split_bitexact(H, W, expect_split):
-    """g_a + g_s forward and input gradient with the inner levels split == row-major, bit for bit (144 x 208 has a
-    17 x 25 third level: the engine keeps g_a row-major; g_s, at 2x / 4x / 8x the latent sides, still splits)."""
+@pytest.mark.parametrize("precision,H,W,expect_split", [("x6", 128, 192, True), ("x6", 64, 96, True),
+                                                        ("x6", 136, 200, False), ("fp32", 128, 192, True),
+                                                        ("bf16", 128, 192, True), ("fp32", 64, 64, True)])
+def test_chain_split_bitexact(precision, H, W, expect_split):
+    """g_a + g_s forward and input gradient with the inner levels split == row-major, bit for bit, on every
+    operand path (the fp32 64 x 64 case runs the small-grid kernels).  136 x 200 has a 17 x 25 third level: the
+    engine keeps g_a row-major there; g_s, at 2x / 4x / 8x the latent sides, still splits."""
     from imagecompression_adversarial_amd import hip_ops as K
     P = codec.perturb_params(codec.init_params("hyper", 3, seed=0), seed=1)
-    ks, kr = _kern(P), _kern(P)
-    assert ks.ga.split and ks.gs.split
+    ks, kr = _kern(P, precision), _kern(P, precision)
+    ks.ga.split = ks.gs.split = True   # every inner level, whatever the path's default policy
     kr.ga.split = kr.gs.split = False
     g = torch.Generator().manual_seed(3)
     x = torch.rand((2, 3, H, W), generator=g).to(DEV)
@@ -188,7 +193,7 @@ def test_chain_split_bitexact(H, W, expect_split):
             gx4 = gy4
         else:
             gx4 = k.g_a_backward(gy4, sa)
-        res.append((y4, xh4, gx4, sa.split, ss.split))
+        res.append((y4, xh4, gx4, any(sa.split), any(ss.split)))
     assert res[0][3] == expect_split and res[0][4]
     assert not res[1][3] and not res[1][4]
     for a, b in zip(res[0][:3], res[1][:3]):
@@ -207,3 +212,11 @@ def test_attack_split_bitexact():
     assert a.branches == b.branches
     _same(a.noise, b.noise)
     _same(a.output_s, b.output_s)
+
+
+def test_split_policy():
+    """The default per-level choice (engine._split_policy): x6 splits L1-L3, bf16 L2-L3, fp32 none."""
+    P = codec.perturb_params(codec.init_params("hyper", 3, seed=0), seed=1)
+    for precision, want in (("x6", (True, True, True)), ("bf16", (False, True, True)), ("fp32", (False,) * 3)):
+        k = _kern(P, precision)
+        assert k.ga.split == want and k.gs.split == want, precision
