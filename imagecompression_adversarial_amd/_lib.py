@@ -79,6 +79,12 @@ _SIGS = {
     "ica_pmf_to_quantized_cdf": [_p, _i, _i, _p],
     "ica_rans_encode": [_p, _p, _l, _p, _i, _p, _p, _i, _p, _l, _p],
     "ica_rans_decode": [_p, _l, _p, _l, _p, _i, _p, _p, _i, _p],
+    "ica_rans_dec_open": [_p, _l, _p],
+    "ica_rans_dec_step": [_p, _i, _p, _l, _p, _i, _p, _p, _i, _p, _p],
+    "ica_rans_dec_close": [_p],
+    # autoregressive coding of the context models (ica_ar.hip)
+    "ica_ar_lds_bytes": [_i, _i, _i],
+    "ica_ar_step": [_p, _i, _i, _i, _p],
     "ica_round": [_p, _p, _l, _p],
     "ica_clamp01": [_p, _p, _l, _p],
     "ica_sqdiff_partial": [_p, _p, _p, _i, _l, _i, _p],
@@ -108,7 +114,7 @@ _SIGS = {
 }
 _RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_conv_weight_bf16_size": _sz,
              "ica_pack_conv_weight_x6_size": _sz, "ica_pack_gdn_x6_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz,
-             "ica_rans_encode": _l}
+             "ica_rans_encode": _l, "ica_ar_lds_bytes": _sz}
 
 
 
@@ -118,6 +124,14 @@ class ConvArgs(C.Structure):
                                             "save_t", "res", "mask")]
                 + [(n, C.c_int) for n in ("N", "Cin", "Hin", "Win", "Cout", "Hout", "Wout", "kind", "KS", "S", "epi",
                                            "it", "fill_mode", "ps", "prec", "layout")])
+
+
+class ArArgs(C.Structure):
+    """include/ica_hip.h ica_ar_args."""
+    _fields_ = ([(n, C.c_void_p) for n in ("y", "params", "yhat", "sym", "idx", "sym_in", "means", "wc", "bc", "w1",
+                                            "b1", "w2", "b2", "w3", "b3", "table")]
+                + [("T", C.c_int), ("bound", C.c_float)]
+                + [(n, C.c_int) for n in ("B", "M", "H", "W", "E1", "E2")])
 
 
 _lib = None

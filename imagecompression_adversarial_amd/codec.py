@@ -768,6 +768,60 @@ class ScaleHyperprior(CompressionModel):
             return {"x_hat": K.from_nc4(xh4, 3).clamp_(0, 1)}
 
 
+def _ar_coder(model):
+    """The model's packed context-model coder (ar_coding.ArCoder), rebuilt when a parameter changes."""
+    from .ar_coding import ArCoder
+    key = tuple((p.data_ptr(), p._version) for p in model.parameters())
+    cache = getattr(model, "_ar_cache", None)
+    if cache is None or cache[0] != key:
+        gc = model.gaussian_conditional
+        sd = {k: v.detach() for k, v in model.state_dict().items()}
+        cache = (key, ArCoder(sd, model.M, gc.scale_table.to(model.entropy_bottleneck.quantiles.device),
+                              float(gc.scale_bound)))
+        model._ar_cache = cache
+    return cache[1]
+
+
+def _ar_compress(model, x):
+    """JointAutoregressiveHierarchicalPriors.compress: z -> EntropyBottleneck bitstreams, params = h_s(z_hat), y ->
+    the autoregressive GaussianConditional bitstreams (ar_coding; position-major symbols, one stream per image)."""
+    from . import entropy_coding as EC_
+    B, _, H, W = x.shape
+    if H % 64 or W % 64:
+        raise ValueError(f"{H}x{W}: the context models code images whose sides are multiples of 64 "
+                         "(y is then exactly 4x the hyper-latent grid)")
+    eb, gc = model.entropy_bottleneck, model.gaussian_conditional
+    ztab, ytab = eb._coder_tables(), gc._coder_tables()
+    ck = model.kernels()
+    with torch.no_grad():
+        x4 = K.to_nc4(x.detach().contiguous())
+        y4, _ = ck.ga.forward(x4)
+        z4 = ck.ha.forward(y4)
+        _, _, zh, zw, _ = z4.shape
+        med = eb._get_medians().detach().reshape(-1).contiguous()
+        zs, zi = EC_.eb_symbols(z4, model.N, med)
+        z_hat4 = EC_.dequantize(zs, B, model.N, zh, zw, medians=med, device=x.device)
+        params4 = ck.hs.forward(z_hat4)
+        ys, yi, _ = _ar_coder(model).encode(y4, params4)
+        z_strings = EC_.encode_batch(zs, zi, ztab)
+        y_strings = EC_.encode_batch(ys, yi, ytab)
+    return {"strings": [y_strings, z_strings], "shape": torch.Size((zh, zw))}
+
+
+def _ar_decompress(model, strings, shape):
+    """JointAutoregressiveHierarchicalPriors.decompress: z_hat, params = h_s(z_hat), y_hat position by position,
+    x_hat = g_s(y_hat).clamp(0, 1)."""
+    eb, gc = model.entropy_bottleneck, model.gaussian_conditional
+    ytab = gc._coder_tables()
+    ck = model.kernels()
+    with torch.no_grad():
+        z_hat = eb.decompress(strings[1], shape)
+        params4 = ck.hs.forward(K.to_nc4(z_hat))
+        y_hat4 = _ar_coder(model).decode(strings[0], params4, ytab)
+        xh4, _ = ck.gs.forward(y_hat4)
+        return {"x_hat": K.from_nc4(xh4, 3).clamp_(0, 1)}
+
+
 class Cheng2020Anchor(CompressionModel):
     """compressai.models.Cheng2020Anchor (JointAutoregressiveHierarchicalPriors with residual transforms).
     Eval-mode forward (the attack path); training this model is out of scope."""
@@ -793,6 +847,12 @@ class Cheng2020Anchor(CompressionModel):
         return {"x_hat": K.from_nc4(res["x_hat4"], 3),
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
 
+    def compress(self, x):
+        return _ar_compress(self, x)
+
+    def decompress(self, strings, shape):
+        return _ar_decompress(self, strings, shape)
+
 
 class JointAutoregressiveHierarchicalPriors(CompressionModel):
     """compressai.models.JointAutoregressiveHierarchicalPriors (mbt2018): bmshj2018 g_a / g_s, LReLU hyper
@@ -817,6 +877,12 @@ class JointAutoregressiveHierarchicalPriors(CompressionModel):
         res = self.kernels().forward(K.to_nc4(x.detach().contiguous()))
         return {"x_hat": K.from_nc4(res["x_hat4"], 3),
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
+
+    def compress(self, x):
+        return _ar_compress(self, x)
+
+    def decompress(self, strings, shape):
+        return _ar_decompress(self, strings, shape)
 
 
 # --------------------------------------------------------------------------- #

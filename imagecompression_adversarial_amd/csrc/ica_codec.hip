@@ -249,24 +249,36 @@ long ica_rans_encode(const int32_t* symbols, const int32_t* indexes, long n, con
   return nbytes;
 }
 
-// Decode n symbols (the inverse of ica_rans_encode with the same indexes / tables).  Returns 0, -5 on a
-// bad index / table, -8 when the stream ends early (truncated or corrupt input).
-int ica_rans_decode(const uint8_t* data, long nbytes, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
-                    const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols) {
+// One bitstream's decoder state: the words, the read position and the 64-bit rANS state.  Decoding can stop after
+// any symbol and resume with the next call (the context models decode one latent position at a time, because the
+// next position's CDF rows depend on the symbols just decoded).
+struct RansDec {
+  std::vector<uint32_t> words;
+  size_t pos = 0;
+  uint64_t x = 0;
+};
+
+static int rans_dec_init(RansDec& d, const uint8_t* data, long nbytes) {
   if (nbytes < 8 || (nbytes & 3)) return -8;
-  std::vector<uint32_t> words((size_t)nbytes / 4);
-  std::memcpy(words.data(), data, (size_t)nbytes);
-  const uint32_t* p = words.data();
-  const uint32_t* const end = p + words.size();
-  uint64_t x = (uint64_t)p[0] | ((uint64_t)p[1] << 32);
-  p += 2;
+  d.words.resize((size_t)nbytes / 4);
+  std::memcpy(d.words.data(), data, (size_t)nbytes);
+  d.x = (uint64_t)d.words[0] | ((uint64_t)d.words[1] << 32);
+  d.pos = 2;
+  return 0;
+}
+
+static int rans_dec_run(RansDec& d, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
+                        const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols) {
+  const size_t end = d.words.size();
   const uint32_t mask = (1u << kPrec) - 1;
+  uint64_t x = d.x;
+  size_t p = d.pos;
   auto get_bits = [&](uint32_t nb, uint32_t& v) -> bool {
     v = (uint32_t)(x & ((1u << nb) - 1));
     x >>= nb;
     if (x < kRansL) {
       if (p >= end) return false;
-      x = (x << 32) | *p++;
+      x = (x << 32) | d.words[p++];
     }
     return true;
   };
@@ -285,7 +297,7 @@ int ica_rans_decode(const uint8_t* data, long nbytes, const int32_t* indexes, lo
     x = freq * (x >> kPrec) + (x & mask) - start;
     if (x < kRansL) {
       if (p >= end) return -8;
-      x = (x << 32) | *p++;
+      x = (x << 32) | d.words[p++];
     }
     int32_t value = s;
     if (value == max_value) {
@@ -307,6 +319,51 @@ int ica_rans_decode(const uint8_t* data, long nbytes, const int32_t* indexes, lo
     }
     symbols[i] = value + offsets[k];
   }
+  d.x = x;
+  d.pos = p;
+  return 0;
+}
+
+// Decode n symbols (the inverse of ica_rans_encode with the same indexes / tables).  Returns 0, -5 on a
+// bad index / table, -8 when the stream ends early (truncated or corrupt input).
+int ica_rans_decode(const uint8_t* data, long nbytes, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
+                    const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols) {
+  RansDec d;
+  if (const int rc = rans_dec_init(d, data, nbytes)) return rc;
+  return rans_dec_run(d, indexes, n, cdfs, stride, cdf_sizes, offsets, n_cdfs, symbols);
+}
+
+// Incremental decoding (the context models): open a decoder on one bitstream (*decoder = NULL and -8 for a
+// malformed one), decode n symbols of each of B open decoders per call (indexes / symbols [B][n]; returns 0 or the
+// first error, the failing image in *bad), close.
+int ica_rans_dec_open(const uint8_t* data, long nbytes, void** decoder) {
+  RansDec* d = new RansDec;
+  if (const int rc = rans_dec_init(*d, data, nbytes)) {
+    delete d;
+    *decoder = nullptr;
+    return rc;
+  }
+  *decoder = d;
+  return 0;
+}
+
+int ica_rans_dec_step(void* const* decoders, int B, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
+                      const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols, int* bad) {
+  for (int b = 0; b < B; ++b) {
+    RansDec* d = static_cast<RansDec*>(decoders[b]);
+    const int rc = d ? rans_dec_run(*d, indexes + (long)b * n, n, cdfs, stride, cdf_sizes, offsets, n_cdfs,
+                                    symbols + (long)b * n)
+                     : -8;
+    if (rc != 0) {
+      if (bad) *bad = b;
+      return rc;
+    }
+  }
+  return 0;
+}
+
+int ica_rans_dec_close(void* decoder) {
+  delete static_cast<RansDec*>(decoder);
   return 0;
 }
 

@@ -138,6 +138,50 @@ long ica_rans_encode(const int32_t* symbols, const int32_t* indexes, long n, con
                      long* needed);
 int ica_rans_decode(const uint8_t* data, long nbytes, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
                     const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols);
+/* Incremental decoding (context models: one latent position of every image per call, because the next position's
+ * CDF rows depend on the symbols just decoded).  open: *decoder = a decoder over one bitstream (-8 and NULL for a
+ * malformed one); step: n symbols from each of B decoders (indexes / symbols [B][n]; the first error, its image in
+ * *bad); close frees one decoder. */
+int ica_rans_dec_open(const uint8_t* data, long nbytes, void** decoder);
+int ica_rans_dec_step(void* const* decoders, int B, const int32_t* indexes, long n, const int32_t* cdfs, int stride,
+                      const int32_t* cdf_sizes, const int32_t* offsets, int n_cdfs, int32_t* symbols, int* bad);
+int ica_rans_dec_close(void* decoder);
+
+/* Autoregressive coding of the context models' latents (mbt2018 / cheng2020; CompressAI
+ * JointAutoregressiveHierarchicalPriors._compress_ar / _decompress_ar, anchors/model.py:97-106): one workgroup
+ * per image walks the latent raster; per position the type-A 5x5 masked context conv over the 12 causal taps of
+ * the zero-padded y_hat, entropy_parameters (1x1: 4M -> E1 -> E2 -> 2M, LeakyReLU 0.01), scales / means, CDF row
+ * index (as ica_gc_symbols) and, encoding, symbol = round(y - mean), y_hat = symbol + mean.
+ *   y, params  nChw4c latents [B][M/4][H][W][4] and h_s output [B][2M/4][H][W][4]
+ *   yhat       [B][M][H+4][W+4] float, zero-initialised by the caller (the padded y_hat)
+ *   sym, idx   mode 0: [B][H W M] (position-major, the bitstream order); mode 1: idx [B][M] of position p0
+ *   sym_in     mode 1: [B][M] decoded symbols of position p0 - 1 (applied first when p0 > 0); means [B][M]
+ *   wc [2M][12M] (k = tap * M + c, taps: rows 0-1 of the window, then row 2 columns 0-1), bc [2M],
+ *   w1 [E1][4M], w2 [E2][E1], w3 [2M][E2] and biases: the entropy_parameters 1x1 weights
+ * mode 0 encodes positions [p0, p1); mode 1 is one decode step (p1 <= p0 + 1).  Returns 0, -2 bad sizes, -4 mode. */
+typedef struct ica_ar_args {
+  const float* y;
+  const float* params;
+  float* yhat;
+  int32_t* sym;
+  int32_t* idx;
+  const int32_t* sym_in;
+  float* means;
+  const float* wc;
+  const float* bc;
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const float* b2;
+  const float* w3;
+  const float* b3;
+  const float* table;
+  int T;
+  float bound;
+  int B, M, H, W, E1, E2;
+} ica_ar_args;
+size_t ica_ar_lds_bytes(int M, int E1, int E2);
+int ica_ar_step(const ica_ar_args* args, int p0, int p1, int mode, hipStream_t stream);
 /* y = conv2d(x, W, stride S, pad KS/2) (+ epilogue).  KS,S in {(5,2),(3,1)}.
  * GDN/IGDN: gp = gamma' fragments, beta = beta_eff, optional save_x/save_s outputs;
  * GDN_BWD/IGDN_BWD: x holds dL/d(conv output of the NEXT layer's input) ... i.e. acc = dL/dy of a GDN,

@@ -206,3 +206,32 @@ def rans_decode(data: bytes, indexes, cdfs, cdf_sizes, offsets):
             value = -value - 1 if raw & 1 else value + max_value
         out.append(value + int(offsets[k]))
     return out
+
+
+def compress_ar_symbols(P, y, params, scale_table, bound=0.11):
+    """JointAutoregressiveHierarchicalPriors._compress_ar (compressai/models/google.py; the context models the
+    reference builds at anchors/model.py:74-77, entropy estimated at anchors/model.py:97-106), for every image of
+    y [B, M, H, W] with params = h_s(z_hat) [B, 2M, H, W]: raster order; y_crop = the 5x5 window of the zero-padded
+    y_hat; ctx = conv2d(y_crop, masked weight, bias); gaussian_params = entropy_parameters(cat(params, ctx));
+    scales, means = chunk(2); index = build_indexes(scales); symbol = round(y - means); y_hat = symbol + means.
+    Returns (symbols, indexes) [B, H W M] int32 in the bitstream's position-major order and y_hat [B, M, H, W].
+    Pure-Python loop over positions: small latents only."""
+    from .codec import context_mask, entropy_parameters
+    B, M, H, W = y.shape
+    w = P["context_prediction.weight"] * context_mask(P["context_prediction.weight"].shape[-1])
+    pad = 2
+    y_hat = torch.nn.functional.pad(y, (pad, pad, pad, pad))
+    syms = torch.empty((B, H * W, M), dtype=torch.int32)
+    idxs = torch.empty_like(syms)
+    for h in range(H):
+        for x in range(W):
+            crop = y_hat[:, :, h:h + 5, x:x + 5]
+            ctx = torch.nn.functional.conv2d(crop, w, P["context_prediction.bias"])
+            gp = entropy_parameters(P, torch.cat((params[:, :, h:h + 1, x:x + 1], ctx), dim=1))
+            scales, means = gp.chunk(2, 1)
+            idx = build_indexes(scales, scale_table, bound).reshape(B, M)
+            q = torch.round(crop[:, :, pad, pad] - means.reshape(B, M)).int()
+            y_hat[:, :, h + pad, x + pad] = q.float() + means.reshape(B, M)
+            syms[:, h * W + x] = q
+            idxs[:, h * W + x] = idx.int()
+    return syms.reshape(B, -1), idxs.reshape(B, -1), y_hat[:, :, pad:-pad, pad:-pad]
