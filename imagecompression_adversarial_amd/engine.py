@@ -57,17 +57,14 @@ def _levels(split):
 
 
 def _split_policy(convs):
-    """Which inner levels (L1, L2, L3) of the k5 s2 stacks are stored parity-split (§3e).  Every conv kernel
-    addresses that order (ica_conv_args.layout), so this is a measured choice per operand path (config-2 / config-5
-    shapes): x6 gains on every level (the conv_up stores and GDN-backward reads are dense, and the x6 conv_up3 and
-    RGB-end kernels are indifferent); bf16 gains on L2 / L3 but its RGB-end kernels (the RGB GDN forward store,
-    the Z-gather loads) lose more than the L1 conv_up launches gain; the fp32 kernels are MFMA-bound, the split's
-    address arithmetic costs ~1 %."""
+    """Which inner levels (L1, L2, L3) of the k5 s2 stacks are stored parity-split.  Every conv
+    kernel addresses that order (ica_conv_args.layout), so this is a measured choice per operand path: x6 and bf16
+    store all three split (config 2: 1351 -> 1371 img-step/s; config 5: 390 -> 394, where the L1 conv_up launches
+    gain 1.6 ms and the bf16 RGB-end kernels give back 0.7 of it; L1 row-major measured 393); the fp32 kernels are
+    MFMA-bound and the split's address arithmetic cost them 0.5 % (779 -> 775), so fp32 stays row-major."""
     precs = {c.fwd_prec for c in convs} | {c.bwd_prec for c in convs}
-    if precs == {K.PREC_X6}:
+    if precs & {K.PREC_X6, K.PREC_BF16}:
         return (True, True, True)
-    if K.PREC_BF16 in precs:
-        return (False, True, True)
     return (False, False, False)
 
 

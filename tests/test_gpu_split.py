@@ -220,8 +220,8 @@ def test_attack_split_bitexact():
 
 
 def test_split_policy():
-    """The default per-level choice (engine._split_policy): x6 splits L1-L3, bf16 L2-L3, fp32 none."""
+    """The default per-level choice (engine._split_policy): x6 and bf16 split L1-L3, fp32 none."""
     P = codec.perturb_params(codec.init_params("hyper", 3, seed=0), seed=1)
-    for precision, want in (("x6", (True, True, True)), ("bf16", (False, True, True)), ("fp32", (False,) * 3)):
+    for precision, want in (("x6", (True, True, True)), ("bf16", (True, True, True)), ("fp32", (False,) * 3)):
         k = _kern(P, precision)
         assert k.ga.split == want and k.gs.split == want, precision
