@@ -50,7 +50,7 @@ def gdn_param_grads(raw_beta, raw_gamma, t4, saved, C, g_beta, g_gamma):
 
 
 def _row_major(saved):
-    if getattr(saved, "split", False):
+    if any(getattr(saved, "split", ())):
         raise RuntimeError("parameter gradients need the forward's activations row-major (forward(..., split=False))")
 
 
