@@ -4,9 +4,6 @@
 // Reference anchors: anchors/utils.py:112-130 (conv / deconv geometry), utils/ops.py:58-97 (GDN).
 #pragma once
 #include "ica_common.h"
-#ifndef ICA_X6_RCP
-#define ICA_X6_RCP 0
-#endif
 
 enum {
   EPI_BIAS = 0,      // y = acc + bias
@@ -531,12 +528,10 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const f32x4 yv = X6 ? yq[X6 ? it : 0][g] : IX.ld(vo_ld, ss), sv = X6 ? sq[X6 ? it : 0][g] : IS.ld(vo_ld, ss);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            // x6: one v_rcp_f32 instead of two IEEE divisions (as gdn_bwd_x6_wide)
-            const float sg = sv[e], rs = X6 && ICA_X6_RCP ? __builtin_amdgcn_rcpf(sg) : 0.f;
-            const float xs = X6 && ICA_X6_RCP ? yv[e] * rs : yv[e] / sg;
+            const float sg = sv[e];
+            const float xs = yv[e] / sg;
             const float gx = acc[it][4 * g + e] * xs;
-            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg)
-                                                  : (X6 && ICA_X6_RCP ? (0.5f * gx) * rs : gx / (2.0f * sg));
+            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
             if constexpr (X6 == 1) tw[4 * (g & 1) + e] = tv;
             else tt[it][4 * g + e] = tv;
             float gs = acc[it][4 * g + e] * sg;

@@ -1,5 +1,8 @@
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
-bash scripts/gpu_evidence.sh c2 32 512 768 x6 --mixed 40 \
-&& timeout -k 10 600 python bench.py --config 3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab/bench_c3.log 2>&1 && echo c3 ok \
-&& timeout -k 10 600 python bench.py --config 4 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab/bench_c4.log 2>&1 && echo c4 ok
+V=scripts/variants
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread -s"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_cheng.py tests/test_gpu_mbt.py -m gpu > gpurun_out/ab/pytest_cheng2.log 2>&1 && echo cheng ok; \
+bash scripts/gpu_ab.sh scripts/kbench_x6.py "x6 " base $V/librcp.so > gpurun_out/ab/rcp.log 2>&1 && echo ab ok \
+&& ICA_HIP_LIB=$V/librcp.so timeout -k 10 600 $T tests/test_traj100.py tests/test_gpu_x6.py -m gpu > gpurun_out/ab/pytest_rcp.log 2>&1 && echo rcp tests ok; \
+timeout -k 10 700 python scripts/cheng_seed_sweep.py 24 > gpurun_out/ab/cheng_sweep.log 2>&1 && echo sweep ok

@@ -7,7 +7,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import attack as oa          # noqa: E402  (checker only)
 from oracle import codec as oc           # noqa: E402
 from imagecompression_adversarial_amd.attack import attack_batch              # noqa: E402
