@@ -528,10 +528,12 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           const f32x4 yv = X6 ? yq[X6 ? it : 0][g] : IX.ld(vo_ld, ss), sv = X6 ? sq[X6 ? it : 0][g] : IS.ld(vo_ld, ss);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float sg = sv[e];
-            const float xs = yv[e] / sg;
+            // x6: one v_rcp_f32 (1 ulp) replaces the two IEEE divisions (measured 2.7% on up.gdn_bwd)
+            const float sg = sv[e], rs = X6 ? __builtin_amdgcn_rcpf(sg) : 0.f;
+            const float xs = X6 ? yv[e] * rs : yv[e] / sg;
             const float gx = acc[it][4 * g + e] * xs;
-            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
+            const float tv = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg)
+                                                  : (X6 ? (0.5f * gx) * rs : gx / (2.0f * sg));
             if constexpr (X6 == 1) tw[4 * (g & 1) + e] = tv;
             else tt[it][4 * g + e] = tv;
             float gs = acc[it][4 * g + e] * sg;
