@@ -1,0 +1,141 @@
+"""Float64 replay of the oracle attack with the per-step gradients recorded (test infrastructure).
+
+Used to show where an fp32-level attack trajectory may leave the float64 one: Adam divides each gradient element
+by its own running RMS, so an element whose exact gradient is, at some step, within fp32 rounding of zero
+(|g| <~ 1e-4 of the step's max|g| here) has an ill-determined update, while every other element follows the
+float64 trajectory to fp32 accuracy (oracle/attack.py:122-176 follows attack_rd.py:486-560)."""
+import torch
+
+from oracle import attack as oa
+
+
+class _RecordingAdam(torch.optim.Adam):
+    """torch.optim.Adam that keeps, per step, the gradient, the state it starts from (noise, exp_avg, exp_avg_sq)
+    and the noise it produces."""
+    log = None
+
+    def step(self, closure=None):
+        (p,) = self.param_groups[0]["params"]
+        st = self.state.get(p, {})
+        z = torch.zeros_like(p)
+        rec = {"grad": p.grad.detach().clone(), "noise": p.detach().clone(),
+               "m": st.get("exp_avg", z).detach().clone(), "v": st.get("exp_avg_sq", z).detach().clone()}
+        out = super().step(closure)
+        rec["noise_next"] = p.detach().clone()
+        _RecordingAdam.log.append(rec)
+        return out
+
+
+def attack_with_log(P, x, steps, monkeypatch, **kw):
+    """oa.attack on (P, x) as given (their dtype), returning (result, per-step records)."""
+    _RecordingAdam.log = []
+    with monkeypatch.context() as m:
+        m.setattr(torch.optim, "Adam", _RecordingAdam)
+        res = oa.attack(P, x, steps=steps, **kw)
+    return res, _RecordingAdam.log
+
+
+def replay64(P, x, steps, monkeypatch, with_log=False, **kw):
+    """The float64 trajectory and, per element, min over steps of |g| / max|g| (its conditioning)."""
+    P64 = {k: v.double() for k, v in P.items()}
+    res, log = attack_with_log(P64, x.double(), steps, monkeypatch, **kw)
+    gmin = torch.stack([r["grad"].abs() / r["grad"].abs().max() for r in log]).amin(0)
+    return (res, gmin, log) if with_log else (res, gmin)
+
+
+ILL = 1e-4   # an element is ill-conditioned when its float64 gradient falls below ILL of the step's max
+
+
+def confined(noise, res64, gmin, tol=1e-3):
+    """(elements beyond tol of max|noise64|, of which outside the ill-conditioned set, max deviation)."""
+    d = (noise.double().cpu() - res64.noise).abs() / res64.noise.abs().max()
+    bad = d > tol
+    return int(bad.sum()), int((bad & (gmin >= ILL)).sum()), float(d.max())
+
+
+# --------------------------------------------------------------------------- #
+# Leaky-ReLU kinks: pre-activations within fp32 resolution of zero
+# --------------------------------------------------------------------------- #
+def kinks(P64, x64, rel=1e-6):
+    """[(call index, flat element, |a| / max|a|)] of the leaky-ReLU inputs of cheng_g_s(cheng_g_a(x)) (float64)
+    that sit within rel of zero: an fp32-accurate forward may put them on either side."""
+    from oracle import codec as oc
+    seen = []
+    orig = oc.lrelu
+
+    def rec(a):
+        seen.append(a.detach())
+        return orig(a)
+
+    oc.lrelu = rec
+    try:
+        with torch.no_grad():
+            oc.cheng_g_s(P64, oc.cheng_g_a(P64, x64))
+    finally:
+        oc.lrelu = orig
+    out = []
+    for i, a in enumerate(seen):
+        m = float(a.abs().max())
+        for e in (a.abs().flatten() < rel * m).nonzero().flatten().tolist():
+            out.append((i, e, float(a.flatten()[e].abs()) / m))
+    return out
+
+
+def transforms_flipped(P64, x, flips=()):
+    """cheng_g_s(cheng_g_a(x)) in float64 with the leaky ReLUs of the kinks in flips = [(call index, flat
+    element)] taking their other branch (value and slope)."""
+    from oracle import codec as oc
+    orig = oc.lrelu
+    calls = [0]
+
+    def lr(a):
+        out = orig(a)
+        mine = [e for c, e in (flips or ()) if c == calls[0]]
+        if mine:
+            onehot = torch.zeros(a.numel(), dtype=a.dtype)
+            onehot[mine] = 1.0
+            onehot = onehot.reshape(a.shape)
+            other = torch.where(a > 0, oc.LRELU_SLOPE * a, a)
+            out = out + onehot * (other - out)
+        calls[0] += 1
+        return out
+
+    oc.lrelu = lr
+    try:
+        return oc.cheng_g_s(P64, oc.cheng_g_a(P64, x))
+    finally:
+        oc.lrelu = orig
+
+
+def input_grad_flipped(P64, x, gout, flips=()):
+    """d <gout, transforms(x)> / dx in float64, with kinks flipped (transforms_flipped)."""
+    xr = x.double().clone().requires_grad_(True)
+    transforms_flipped(P64, xr, flips).backward(gout.double())
+    return xr.grad
+
+
+def match_kinks(P64, x64, gout, gx, tol=2e-5, rel=1e-5, max_flips=2):
+    """Per image, the kinks (pre-activations within rel of their tensor's max of zero) with which the float64
+    input gradient matches gx: greedy, at most max_flips per image, each round taking the candidate that lowers
+    the image's max abs error most.  Returns ([flips per image], max abs error / max over the batch); a flip is
+    (call index, flat element of the one-image tensor)."""
+    gx = gx.double().cpu()
+    scale = float(input_grad_flipped(P64, x64, gout).abs().max())
+    flips_all, worst = [], 0.0
+    for b in range(x64.shape[0]):
+        xb, gb, tb = x64[b:b + 1], gout[b:b + 1], gx[b:b + 1]
+
+        def err(fl):
+            return float((tb - input_grad_flipped(P64, xb, gb, fl)).abs().max()) / scale
+
+        cur, e = [], err([])
+        cands = [(c, el) for c, el, _ in kinks(P64, xb, rel)]
+        while e > tol and len(cur) < max_flips:
+            trial = min(((err(cur + [k]), k) for k in cands if k not in cur), default=None)
+            if trial is None or trial[0] >= e:
+                break
+            e, k = trial
+            cur.append(k)
+        flips_all.append(cur)
+        worst = max(worst, e)
+    return flips_all, worst
