@@ -50,8 +50,10 @@ _SIGS = {
     "ica_nc4_to_nchw": [_p, _p, _i, _i, _i, _i, _p],
     "ica_reduce_rows": [_p, _p, _i, _i, _f, _p],
     "ica_attack_prologue": [_p, _p, _p, _p, _i, _i, _i, _f, _p],
+    "ica_attack_prologue_ex": [_p, _p, _p, _p, _i, _i, _i, _f, _i, _p],
     "ica_attack_loss": [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _p],
     "ica_attack_adam": [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _f, _f, _p, _p, _p, _p],
+    "ica_attack_adam_ex": [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _f, _f, _p, _p, _p, _i, _p],
     "ica_branch_select": [_p, _f, _i, _p, _p, _p],
     "ica_gather_images": [_p, _p, _p, _i, _l, _p],
     "ica_roi_prologue": [_p, _p, _p, _p, _i, _i, _i, _f, _i, _i, _i, _i, _f, _f, _p],

@@ -21,9 +21,9 @@ def init_model(MODEL, quality, metric, pretrained=True):
         return codec.cheng2020_anchor(quality=quality, metric=metric, pretrained=pretrained)
     if MODEL == "context":
         return codec.mbt2018(quality=quality, metric=metric, pretrained=pretrained)
-    if MODEL == "debug":
-        raise NotImplementedError("model 'debug' (ae_onelayer) is not on this backend (out of §8 scope); "
-                                  "supported: factorized, hyper, context, cheng2020")
+    if MODEL == "debug":   # anchors/model.py:61-68: ae_onelayer(N=3, M=192) at every quality, never pretrained
+        assert not pretrained, "No download-able model available!"
+        return codec.AeOneLayer(N=3, M=192)
     raise AssertionError(f"'{MODEL}' not in ['factorized', 'hyper', 'context', 'cheng2020', 'debug']")
 
 

@@ -143,7 +143,17 @@ class AttackLoop:
         self.gscale = float(1.0 / (self.B_global * 3 * H * W)) if coupled else self.invN
         self.dval = 1.0 / self.B_global if coupled else 1.0
         dev = im_s.device
-        self.noise = torch.zeros_like(self.im_s) if init_noise is None else init_noise.clone().contiguous()
+        # the debug model (ae_onelayer) attacks an unclamped input from a random start (attack_rd.py:493-494, 514-515)
+        self.clamp_in = bool(getattr(kern, "clamp_input", True))
+        if init_noise is not None:
+            self.noise = init_noise.clone().contiguous()
+        elif not self.clamp_in:
+            r = float(noise_thr) ** 0.5
+            self.noise = torch.empty(tuple(im_s.shape)).uniform_(-r, r).to(dev)
+        else:
+            self.noise = torch.zeros_like(self.im_s)
+        if target is not None and not self.clamp_in:
+            raise NotImplementedError("the targeted / ROI attack is defined for the clamped-input models")
         self.m = torch.zeros_like(self.im_s)
         self.v = torch.zeros_like(self.im_s)
         self.im_in4 = K.empty_nc4(B, 3, H, W, dev)
@@ -271,8 +281,8 @@ class AttackLoop:
         B, H, W = self.B, self.H, self.W
         if self.roi is not None:
             return self._step_roi(i, record_im_in, census)
-        call("ica_attack_prologue", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
-             self.eps, stream())
+        call("ica_attack_prologue_ex", ptr(self.noise), ptr(self.im_s), ptr(self.im_in4), ptr(self.part), B, H, W,
+             self.eps, int(self.clamp_in), stream())
         K.reduce_rows(self.part, B, self.invN, out=self.loss_i)
         if self.coupled:
             D.couple_loss_i(self.loss_i, self.B_global, self.group)
@@ -286,10 +296,10 @@ class AttackLoop:
             _, _, gY = MS.ms_ssim_value_and_grad(self.im_s, im_in, torch.full((B,), -self.dval, device=im_in.device))
             cheap_grad = gY
         bc2s, neg_step = self._adam_scalars(i)
-        call("ica_attack_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(cheap_grad),
+        call("ica_attack_adam_ex", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(cheap_grad),
              ptr(self.m), ptr(self.v), ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr,
              self.gscale, bc2s, neg_step, ptr(self.branch), ptr(self.gpos if idx is not None else None),
-             ptr(self.census), stream())
+             ptr(self.census), int(self.clamp_in), stream())
         self.steps_done += 1
         if census:
             return self.branch.tolist()

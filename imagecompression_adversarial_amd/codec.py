@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from . import engine as E
 from . import engine_cheng as EC
+from . import engine_debug as ED
 from . import hip_ops as K
 
 # --------------------------------------------------------------------------- #
@@ -673,6 +674,8 @@ class CompressionModel(nn.Module):
                 if precision not in ("fp32", "x6"):
                     raise NotImplementedError("the bf16 conv path covers the bmshj2018 transforms")
                 ex = EC.ChengKernels(sd, precision=precision)
+            elif self.model_kind == "debug":
+                ex = ED.DebugKernels(sd, precision=precision)
             else:
                 ex = E.CodecKernels(sd, self.model_kind, precision=precision)
             cache[1][precision] = ex
@@ -852,6 +855,62 @@ class Cheng2020Anchor(CompressionModel):
 
     def decompress(self, strings, shape):
         return _ar_decompress(self, strings, shape)
+
+
+class DebugAnalysisTransform(_FusedSequential):
+    """ae_onelayer g_a = conv(3, M, kernel_size=3, stride=1) (anchors/model.py:13-15)."""
+
+    def __init__(self, M):
+        super().__init__(conv(3, M, kernel_size=3, stride=1))
+        self.out_channels = M
+
+    def _make_executor(self, sd):
+        return ED.DebugAnalysis(sd, prefix="")
+
+
+class DebugSynthesisTransform(_FusedSequential):
+    """ae_onelayer g_s = deconv(M, 3, kernel_size=3, stride=1) (anchors/model.py:17-19)."""
+
+    def __init__(self, M):
+        super().__init__(deconv(M, 3, kernel_size=3, stride=1))
+        self.out_channels = 3
+
+    def _make_executor(self, sd):
+        return ED.DebugSynthesis(sd, prefix="")
+
+
+class DebugHyperSynthesisTransform(MbtHyperSynthesisTransform):
+    """mbt2018's h_s at N = 3 (z_hat carried at 16 channels, engine_debug.DebugHyperSynthesis)."""
+
+    def _make_executor(self, sd):
+        return ED.DebugHyperSynthesis(sd, prefix="")
+
+
+class AeOneLayer(CompressionModel):
+    """anchors/model.py:8-33 ae_onelayer(MeanScaleHyperprior): one 3x3 stride-1 conv each way around the mean-scale
+    hyperprior; forward reconstructs from the unquantised latent.  No pretrained weights exist (anchors/model.py:62):
+    random / user-supplied weights, eval forward and the attack path (fp32 operands)."""
+    model_kind = "debug"
+
+    def __init__(self, N=3, M=192, **kwargs):
+        super().__init__()
+        self.entropy_bottleneck = EntropyBottleneck(N)
+        self.g_a = DebugAnalysisTransform(M)
+        self.g_s = DebugSynthesisTransform(M)
+        self.h_a = MbtHyperAnalysisTransform(N, M)
+        self.h_s = DebugHyperSynthesisTransform(N, M)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.N, self.M = int(N), int(M)
+
+    def attack_precision(self, requested: str | None = None) -> str:
+        return requested or "fp32"
+
+    def forward(self, x):
+        if self.training:
+            raise NotImplementedError("ae_onelayer training is out of scope on the HIP path (eval forward only)")
+        res = self.kernels("fp32").forward(K.to_nc4(x.detach().contiguous()))
+        return {"x_hat": K.from_nc4(res["x_hat4"], 3),
+                "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
 
 
 class JointAutoregressiveHierarchicalPriors(CompressionModel):

@@ -86,7 +86,8 @@ constexpr int ELEM_BLOCKS_PER_IMAGE = 256;
 // noise_c = Up(Low(noise,-eps),eps); im_in = Up(Low(im_s + noise_c, 0), 1)
 // -> im_in (nChw4c, ch3 = 0) and partial sums of (im_s - im_in)^2.
 __global__ void attack_prologue_kernel(const float* __restrict__ noise, const float* __restrict__ im_s,
-                                       float* __restrict__ im_in4, float* __restrict__ part, long HW, float eps) {
+                                       float* __restrict__ im_in4, float* __restrict__ part, long HW, float eps,
+                                       int clamp_in) {
   __shared__ float sh[4];
   const int b = blockIdx.y;
   const float* nz = noise + (long)b * 3 * HW;
@@ -100,7 +101,7 @@ __global__ void attack_prologue_kernel(const float* __restrict__ noise, const fl
       const float nc = fminf(fmaxf(nz[c * HW + pix], -eps), eps);
       const float s = is[c * HW + pix];
       const float u = fadd_rn(s, nc);
-      const float ii = fminf(fmaxf(u, 0.f), 1.f);
+      const float ii = clamp_in ? fminf(fmaxf(u, 0.f), 1.f) : u;
       v[c] = ii;
       const float d = fsub_rn(s, ii);
       acc = fadd_rn(acc, fmul_rn(d, d));
@@ -233,7 +234,8 @@ __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __res
                                    const float* __restrict__ cheap_grad, float* __restrict__ m,
                                    float* __restrict__ v, float* __restrict__ im_in_out, long HW, float eps,
                                    float thr, float invN, float bc2s, float neg_step, int* __restrict__ branch,
-                                   RoiBox roi, long W, const int* __restrict__ gpos, int* __restrict__ census) {
+                                   RoiBox roi, long W, const int* __restrict__ gpos, int* __restrict__ census,
+                                   int clamp_in) {
   const int b = blockIdx.y;
   const bool cheap = loss_i[b] > thr;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -253,8 +255,8 @@ __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __res
       const float nc = fminf(lowN, eps);
       const float s = im_s[i];
       const float u = fadd_rn(s, nc);
-      const float lowU = fmaxf(u, 0.f);
-      const float ii = fminf(lowU, 1.f);
+      const float lowU = clamp_in ? fmaxf(u, 0.f) : u;
+      const float ii = clamp_in ? fminf(lowU, 1.f) : u;
       if (im_in_out) im_in_out[i] = ii;
       float g;
       if (cheap) {
@@ -269,9 +271,11 @@ __global__ void attack_adam_kernel(float* __restrict__ noise, const float* __res
       } else {
         g = gn[c];
       }
-      // im_in = Up(Low(u, 0), 1)
-      g = (lowU <= 1.f || g > 0.f) ? g : g * 0.f;
-      g = (u >= 0.f || g < 0.f) ? g : g * 0.f;
+      // im_in = Up(Low(u, 0), 1) (clamp_in; the debug model's im_in = u, attack_rd.py:514-515)
+      if (clamp_in) {
+        g = (lowU <= 1.f || g > 0.f) ? g : g * 0.f;
+        g = (u >= 0.f || g < 0.f) ? g : g * 0.f;
+      }
       // noise_c = Up(Low(noise, -eps), eps)
       g = (lowN <= eps || g > 0.f) ? g : g * 0.f;
       g = (nz >= -eps || g < 0.f) ? g : g * 0.f;
@@ -609,12 +613,17 @@ int ica_reduce_rows(const float* part, float* out, int B, int nblk, float scale,
 }
 
 // part must hold B * ica_elem_blocks_per_image() floats.
-int ica_attack_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
-                        float eps, hipStream_t st) {
+int ica_attack_prologue_ex(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
+                           float eps, int clamp_in, hipStream_t st) {
   hipLaunchKernelGGL(attack_prologue_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, im_in4,
-                     part, (long)H * W, eps);
+                     part, (long)H * W, eps, clamp_in);
   ICA_CHECK_LAUNCH();
   return 0;
+}
+
+int ica_attack_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
+                        float eps, hipStream_t st) {
+  return ica_attack_prologue_ex(noise, im_s, im_in4, part, B, H, W, eps, 1, st);
 }
 
 int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float* part, int B, int H, int W,
@@ -625,14 +634,22 @@ int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float*
   return 0;
 }
 
+int ica_attack_adam_ex(float* noise, const float* im_s, const float* gnet4, const float* loss_i,
+                       const float* cheap_grad, float* m, float* v, float* im_in_out, int B, int H, int W, float eps,
+                       float thr, float invN, float bc2s, float neg_step, int* branch, const int* gpos, int* census,
+                       int clamp_in, hipStream_t st) {
+  hipLaunchKernelGGL(attack_adam_kernel<false>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
+                     loss_i, cheap_grad, m, v, im_in_out, (long)H * W, eps, thr, invN, bc2s, neg_step, branch,
+                     RoiBox{}, (long)W, gpos, census, clamp_in);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
 int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
                     float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
                     float bc2s, float neg_step, int* branch, const int* gpos, int* census, hipStream_t st) {
-  hipLaunchKernelGGL(attack_adam_kernel<false>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
-                     loss_i, cheap_grad, m, v, im_in_out, (long)H * W, eps, thr, invN, bc2s, neg_step, branch,
-                     RoiBox{}, (long)W, gpos, census);
-  ICA_CHECK_LAUNCH();
-  return 0;
+  return ica_attack_adam_ex(noise, im_s, gnet4, loss_i, cheap_grad, m, v, im_in_out, B, H, W, eps, thr, invN, bc2s,
+                            neg_step, branch, gpos, census, 1, st);
 }
 
 int ica_roi_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W, float eps,
@@ -660,7 +677,7 @@ int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const floa
   const RoiBox roi{x0, x1, y0, y1, w_in_tar, w_in_bkg, 0.f, 0.f};
   hipLaunchKernelGGL(attack_adam_kernel<true>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
                      loss_i, nullptr, m, v, im_in_out, (long)H * W, eps, thr, 0.f, bc2s, neg_step, branch, roi,
-                     (long)W, gpos, census);
+                     (long)W, gpos, census, 1);
   ICA_CHECK_LAUNCH();
   return 0;
 }

@@ -250,6 +250,10 @@ int ica_reduce_rows(const float* part, float* out, int B, int nblk, float scale,
 /* im_in4 = Up(Low(im_s + Up(Low(noise,-eps),eps), 0), 1) (nChw4c) ; part = per-image partial sum (im_s-im_in)^2. */
 int ica_attack_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
                         float eps, hipStream_t stream);
+/* ica_attack_prologue with clamp_in = 0: im_in4 = im_s + Up(Low(noise,-eps),eps), no [0, 1] clamp (the debug model,
+ * attack_rd.py:514-515). */
+int ica_attack_prologue_ex(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
+                           float eps, int clamp_in, hipStream_t stream);
 /* mode 0: dL/dx_hat of 1 - mean((os - bound01(x_hat))^2) (clamp optional); mode 1: of mean((os - x_hat)^2). */
 int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float* part, int B, int H, int W,
                     float invN, int clamp, int mode, hipStream_t stream);
@@ -257,6 +261,11 @@ int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float*
 int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const float* loss_i, const float* cheap_grad,
                     float* m, float* v, float* im_in_out, int B, int H, int W, float eps, float thr, float invN,
                     float bc2s, float neg_step, int* branch, const int* gpos, int* census, hipStream_t stream);
+/* ica_attack_adam with clamp_in = 0: no [0, 1] bound on im_in, so none in the backward (the debug model). */
+int ica_attack_adam_ex(float* noise, const float* im_s, const float* gnet4, const float* loss_i,
+                       const float* cheap_grad, float* m, float* v, float* im_in_out, int B, int H, int W, float eps,
+                       float thr, float invN, float bc2s, float neg_step, int* branch, const int* gpos, int* census,
+                       int clamp_in, hipStream_t stream);
 /* Branch compaction: sel[0] = E = #images with loss_i <= thr (the network branch, attack_rd.py:334), sel[1..E] =
  * their indexes in order, gpos[b] = row of image b in the compacted sub-batch (-1: cheap branch, no network).
  * ica_attack_adam / ica_roi_adam read the network gradient of image b from row gpos[b] (gpos null: row b) and,

@@ -119,14 +119,22 @@ def attack(P, im_s, steps=1001, epsilon=16.0, noise_thr=1e-4, lr=0.01, att_metri
     if target is not None:
         return _attack_roi(P, im_s, output_s, bpp_ori, steps, noise_range, noise_thr, lr, clamp, model,
                            init_noise, eval_msssim, record, target, roi, la_tar, la_bkg_in, la_bkg_out)
-    noise = torch.zeros_like(im_s) if init_noise is None else init_noise.clone()
+    if init_noise is not None:
+        noise = init_noise.clone()
+    elif model == "debug":   # attack_rd.py:493-494: U(-sqrt(noise), sqrt(noise)) from the global RNG
+        noise = torch.empty(im_s.shape).uniform_(-noise_thr ** 0.5, noise_thr ** 0.5).to(im_s.dtype)
+    else:
+        noise = torch.zeros_like(im_s)
     noise.requires_grad_(True)
     opt = torch.optim.Adam([noise], lr=lr)
     sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1, 2, 3], gamma=0.33)
     im_in = None
     for i in range(steps):
         noise_c = codec.UpBound.apply(codec.LowBound.apply(noise, -noise_range), noise_range)
-        im_in = codec.UpBound.apply(codec.LowBound.apply(im_s + noise_c, 0.0), 1.0)
+        if model == "debug":   # attack_rd.py:514-515: the debug model's input is not clamped to [0, 1]
+            im_in = im_s + noise_c
+        else:
+            im_in = codec.UpBound.apply(codec.LowBound.apply(im_s + noise_c, 0.0), 1.0)
         if coupled:
             loss_i = torch.mean((im_s - im_in) ** 2)
             cheap = torch.full((B,), bool(loss_i > noise_thr))

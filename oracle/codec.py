@@ -40,6 +40,8 @@ def model_channels(model: str, quality: int) -> tuple[int, int]:
     if model == "cheng2020":
         n = 128 if quality <= 3 else 192
         return (n, n)
+    if model == "debug":   # anchors/model.py:61-68: ae_onelayer(N=3, M=192) at every quality
+        return (3, 192)
     raise ValueError(model)
 
 
@@ -250,6 +252,8 @@ def forward(P, x, model="hyper", training=False, noise_y=None, noise_z=None):
     """net(x) -> {"x_hat", "likelihoods": {"y", "z"}} (anchors/balle.py:25-55)."""
     if model == "cheng2020":
         return cheng_forward(P, x, training, noise_y, noise_z)
+    if model == "debug":
+        return debug_forward(P, x, training, noise_y, noise_z)
     if model == "context":
         return mbt_forward(P, x, training, noise_y, noise_z)
     y = g_a(P, x)
@@ -415,10 +419,38 @@ def mbt_forward(P, x, training=False, noise_y=None, noise_z=None):
     return {"x_hat": g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
 
 
+# --------------------------------------------------------------------------- #
+# ae_onelayer, the "debug" model (anchors/model.py:8-33): one 3x3 stride-1 conv each way around the
+# MeanScaleHyperprior entropy model (CompressAI: mbt2018's h_a / h_s, no context model)
+# --------------------------------------------------------------------------- #
+def debug_g_a(P, x):
+    """g_a = conv(3, M, kernel_size=3, stride=1) (anchors/model.py:13-15; anchors/utils.py:112-119)."""
+    return conv(x, P["g_a.0.weight"], P["g_a.0.bias"], stride=1)
+
+
+def debug_g_s(P, y):
+    """g_s = deconv(M, 3, kernel_size=3, stride=1): ConvTranspose2d, padding 1, output_padding 0
+    (anchors/model.py:17-19; anchors/utils.py:122-130)."""
+    return deconv(y, P["g_s.0.weight"], P["g_s.0.bias"], stride=1)
+
+
+def debug_forward(P, x, training=False, noise_y=None, noise_z=None):
+    """ae_onelayer.forward (anchors/model.py:21-33): the likelihoods of the mean-scale hyperprior, and
+    x_hat = g_s(y) -- of the UNQUANTISED latent (the reference's line 30; its y_hat is computed and unused)."""
+    y = debug_g_a(P, x)
+    z = mbt_h_a(P, y)
+    z_hat, z_lik = entropy_bottleneck(P, z, training, noise_z)
+    scales, means = mbt_h_s(P, z_hat).chunk(2, 1)
+    _, y_lik = gaussian_conditional(y, scales, means, training, noise_y)
+    return {"x_hat": debug_g_s(P, y), "likelihoods": {"y": y_lik, "z": z_lik}}
+
+
 def transforms(P, x, model="hyper"):
     """g_s(g_a(x)) without quantisation (the attack's expensive branch, attack_rd.py:344-349)."""
     if model == "cheng2020":
         return cheng_g_s(P, cheng_g_a(P, x))
+    if model == "debug":
+        return debug_g_s(P, debug_g_a(P, x))
     return g_s(P, g_a(P, x))
 
 
@@ -456,6 +488,12 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
 
     if model == "cheng2020":
         return _init_cheng(P, cv, gd, gen, N)
+    if model == "debug":
+        cv("g_a.0", M, 3, 3)
+        cv("g_s.0", 3, M, 3, True)
+        _init_mbt_hyper(cv, N, M)
+        _init_eb(P, gen, N)
+        return P
     cv("g_a.0", N, 3, 5); gd("g_a.1", N)
     cv("g_a.2", N, N, 5); gd("g_a.3", N)
     cv("g_a.4", N, N, 5); gd("g_a.5", N)
@@ -466,12 +504,7 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
     cv("g_s.6", 3, N, 5, True)
     eb_ch = M if model == "factorized" else N
     if model == "context":
-        cv("h_a.0", N, M, 3)
-        cv("h_a.2", N, N, 5)
-        cv("h_a.4", N, N, 5)
-        cv("h_s.0", M, N, 5, True)
-        cv("h_s.2", M * 3 // 2, M, 5, True)
-        cv("h_s.4", M * 2, M * 3 // 2, 3)
+        _init_mbt_hyper(cv, N, M)
         cv("context_prediction", 2 * M, M, 5)
         cv("entropy_parameters.0", M * 10 // 3, M * 12 // 3, 1)
         cv("entropy_parameters.2", M * 8 // 3, M * 10 // 3, 1)
@@ -485,6 +518,16 @@ def init_params(model="hyper", quality=3, seed=0, N=None, M=None):
         cv("h_s.4", M, N, 3)
     _init_eb(P, gen, eb_ch)
     return P
+
+
+def _init_mbt_hyper(cv, N, M):
+    """CompressAI MeanScaleHyperprior / mbt2018 h_a, h_s shapes."""
+    cv("h_a.0", N, M, 3)
+    cv("h_a.2", N, N, 5)
+    cv("h_a.4", N, N, 5)
+    cv("h_s.0", M, N, 5, True)
+    cv("h_s.2", M * 3 // 2, M, 5, True)
+    cv("h_s.4", M * 2, M * 3 // 2, 3)
 
 
 def _init_cheng(P, cv, gd, gen, N):
