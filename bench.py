@@ -461,7 +461,9 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds, model)
+            # cheng2020 on the CPU takes seconds per image-step: its batch variant is 4 images, not the GPU's 32
+            cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds, model,
+                               big_batch=4 if model == "cheng2020" else 32)
         metric = METRIC if model == "hyper" else \
             "attack-step·images/sec, Cheng2020-anchor q6 768×512 (configs[2] per-GPU shard)"
         if roi_mode:
