@@ -1,3 +1,3 @@
 mkdir -p gpurun_out/ab
-bash scripts/gpu_evidence.sh c2 32 512 768 x6 && echo c2 ok \
-&& timeout -k 10 900 python bench.py --config 3 > gpurun_out/ab/c3_bench.log 2>&1 && echo c3 ok
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+timeout -k 10 400 $T tests/test_gpu_attack_cli.py -k debug -m gpu > gpurun_out/ab/pytest_cli.log 2>&1 && echo cli ok

@@ -48,3 +48,13 @@ def test_two_rank_cli_matches_one_rank(tmp_path):
     assert len(pngs) == 9 and pngs == sorted(os.listdir(d2))
     for f in pngs:
         assert (d1 / f).read_bytes() == (d2 / f).read_bytes(), f
+
+
+def test_debug_model_cli(tmp_path):
+    """attack_rd -m debug (ae_onelayer, anchors/model.py:61-68) end to end on the HIP path: seeded synthetic weights
+    (the model has none to download), per-image lines and the AVG line."""
+    cli = ["-m", "imagecompression_adversarial_amd.attack_rd", "-m", "debug", "-q", "3", "-s", "synthetic:2x64x64",
+           "--synthetic-weights", "-steps", "3"]
+    out = _run([sys.executable] + cli, str(tmp_path))
+    lines = _result_lines(out)
+    assert len(lines) == 3 and lines[-1].startswith("AVG:"), out[-2000:]
