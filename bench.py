@@ -461,9 +461,10 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            # cheng2020 on the CPU takes seconds per image-step: its batch variant is 4 images, not the GPU's 32
+            # cheng2020 and the 2048x2048 tiles take seconds per image-step on the CPU: their batch variant is 4 / 2
+            # images, not the GPU's batch (the sample stays at ~1 min of CPU work)
             cpu = cpu_baseline(H, W, args.quality, args.cpu_seconds, model,
-                               big_batch=4 if model == "cheng2020" else 32)
+                               big_batch=4 if model == "cheng2020" else (2 if roi_mode else 32))
         metric = METRIC if model == "hyper" else \
             "attack-step·images/sec, Cheng2020-anchor q6 768×512 (configs[2] per-GPU shard)"
         if roi_mode:
