@@ -175,6 +175,75 @@ def _kernel_table(hook, flops_img):
     return tot_ms, tot_fl
 
 
+def _launch_table(launches, rank):
+    """{tag: [[kernel, grid_threads], ...]} of the timed launches; written to $ICA_LAUNCH_TABLE (rank 0) for
+    scripts/pmc_traffic.py, which matches PMC rows to tags through it."""
+    table = {t: sorted([list(k) for k in v if k]) for t, v in (launches or {}).items()}
+    path = os.environ.get("ICA_LAUNCH_TABLE")
+    if path and rank == 0:
+        with open(path, "w") as f:
+            json.dump(table, f, indent=1)
+    return table
+
+
+def _traffic(tfile, dom, table):
+    """HBM bytes per launch of the dominant tag from the committed PMC file, reported only when its stamp (kernel,
+    grid, source hash: scripts/pmc_traffic.py) matches the launch just timed; otherwise None and the reason."""
+    from imagecompression_adversarial_amd import hip_ops as K
+    if not tfile:
+        return None, "no PMC traffic file for this configuration"
+    tf = os.path.join(REPO, "profiles", tfile)
+    if not os.path.exists(tf):
+        return None, f"profiles/{tfile} absent"
+    try:
+        e = json.load(open(tf)).get(dom)
+    except (OSError, ValueError):
+        return None, f"profiles/{tfile} unreadable"
+    if not isinstance(e, dict):
+        return None, f"profiles/{tfile} has no stamped entry for {dom}"
+    launched = table.get(dom, [])
+    if len(launched) != 1:
+        return None, f"{dom} ran {len(launched)} distinct kernels / grids in the timed steps"
+    kern, grid = launched[0]
+    src = K.source_hash()
+    if e.get("kernel") != kern or e.get("grid") != grid or e.get("src") != src:
+        return None, (f"stale: profiles/{tfile} measured {e.get('kernel')} grid {e.get('grid')} src {e.get('src')}; "
+                      f"timed {kern} grid {grid} src {src}")
+    return e["bytes"], f"profiles/{tfile}: {kern}, grid {grid}, src {src}"
+
+
+def cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner, seconds):
+    """configs[3] on the CPU oracle (oracle.attack.adv_train_step: coupled inner attack + train-mode RD step + clip +
+    Adam + aux Adam), bounded: one outer step with 1 inner step and one with 3, on the bench's batch; the inner-step
+    time is their difference / 2, the rest is the train step, and the rate is that of an outer step with `inner`
+    inner steps (the same accounting as the GPU value: inner image-steps per second of whole outer steps)."""
+    from oracle import attack as oa
+    from oracle import codec
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0)))))
+    P = codec.init_params("hyper", q, seed=0)
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand((B, 3, H, W), generator=g)
+    N, M = codec.model_channels("hyper", q)
+
+    def outer(k):
+        ny = torch.rand((B, M, H // 16, W // 16), generator=g) - 0.5
+        nz = torch.rand((B, N, H // 64, W // 64), generator=g) - 0.5
+        t0 = time.perf_counter()
+        oa.adv_train_step(P, x, steps=k, model="hyper", metric=metric, lmbda=lmbda, noise_y=ny, noise_z=nz)
+        return time.perf_counter() - t0
+    outer(1)   # warm-up
+    t1, t3 = outer(1), outer(3)
+    t_inner = max((t3 - t1) / 2, 1e-9)
+    t_train = max(t1 - t_inner, 0.0)
+    t_outer = inner * t_inner + t_train
+    return {"value": B * inner / t_outer, "unit": "attack-step·images/s", "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": _cpu_model(),
+            "sample": f"oracle adv_train_step (train.py:335-366) on {B} x {W}x{H}, hyper q{q}, {metric}: outer steps "
+                      f"with 1 and 3 inner steps timed ({t1:.1f} s, {t3:.1f} s): {t_inner:.2f} s per inner step, "
+                      f"{t_train:.2f} s train step, extrapolated to {inner} inner steps per outer step "
+                      f"({t_outer:.0f} s)"}
+
+
 def bench_finetune(args):
     """configs[3]: train.py --adv (train.py:335-366) outer steps on this rank's shard: the batch-coupled
     300-step inner attack (a 4-byte all-reduce per inner step), the train-mode RD forward / backward with
@@ -212,6 +281,7 @@ def bench_finetune(args):
     K.EVENT_HOOK = {}
     K.FLOPS_HOOK = {}
     K.PREC_HOOK = {}
+    K.LAUNCH_HOOK = {}
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         adv_step(net, tr, opt, aux, xs[i], fargs, group, world)
@@ -220,6 +290,8 @@ def bench_finetune(args):
         dist.barrier()
     el = time.perf_counter() - t0
     hook, K.EVENT_HOOK = K.EVENT_HOOK, None
+    table = _launch_table(K.LAUNCH_HOOK, rank)
+    K.LAUNCH_HOOK = None
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -236,9 +308,10 @@ def bench_finetune(args):
             return None
         ach = tot_fl[tag] / (tot_ms[tag] * 1e-3) / 1e12
         pk = _peak(K.PREC_HOOK.get(tag, 0))   # the operands that tag's launches ran on
+        traffic, tnote = _traffic("pmc_traffic_c4.json", tag, table)
         return {"bound": "mfma", "kernel": tag, "achieved": round(ach, 2), "peak": pk,
-                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": None, "operands": _PREC_NAME[
-                    K.PREC_HOOK.get(tag, 0)],
+                "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": traffic, "traffic_source": tnote,
+                "operands": _PREC_NAME[K.PREC_HOOK.get(tag, 0)],
                 "launch_ms": round(tot_ms[tag] / len(hook[tag]), 4),
                 "flops_per_launch": tot_fl[tag] / len(hook[tag])}
     ms_outer = el / args.steps * 1e3
@@ -260,7 +333,8 @@ def bench_finetune(args):
             "outer_steps_per_s": round(args.steps / el, 4),
             "roofline": roof(dom), "wgrad_roofline": roof(wdom),
             "per_kernel_ms_total_per_outer_step": {k: round(v / args.steps, 3) for k, v in sorted(tot_ms.items())},
-            "cpu_baseline": None,
+            "cpu_baseline": (None if world > 1 or args.no_cpu_baseline else
+                             cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner, args.cpu_seconds)),
         }
         print(json.dumps(out), flush=True)
     if dist:
@@ -365,6 +439,7 @@ def main():
     K.EVENT_HOOK = {}
     K.PREC_HOOK = {}
     K.FLOPS_HOOK = {}
+    K.LAUNCH_HOOK = {}
     exp0 = loop.expensive_image_steps()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -375,6 +450,8 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     hook, K.EVENT_HOOK = K.EVENT_HOOK, None
+    table = _launch_table(K.LAUNCH_HOOK, rank)
+    K.LAUNCH_HOOK = None
     exp_steps = loop.expensive_image_steps() - exp0   # image-steps of the timed window that ran the network
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -397,8 +474,8 @@ def main():
     tag_prec = (dict(K.PREC_HOOK) or _tag_prec(kern)) if model == "hyper" else dict(K.PREC_HOOK)
     peak = _peak(tag_prec.get(dom, 0))
     # HBM bytes per launch of the dominant kernel from the committed PMC passes of the same shapes
-    # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction)
-    traffic = None
+    # (scripts/gpu_pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction), only
+    # when the file's stamp names the kernel, grid and sources just timed
     tfile = None
     if args.precision == "x6" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "hyper":
         tfile = "pmc_traffic_x6.json"
@@ -408,12 +485,7 @@ def main():
         tfile = "pmc_traffic_c5.json"
     elif args.precision == "x6" and not roi_mode and (H, W, B) == (512, 768, 32) and model == "cheng2020":
         tfile = "pmc_traffic_c3x6.json"
-    tf = os.path.join(REPO, "profiles", tfile) if tfile else None
-    if tf and os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(dom)
-        except Exception:
-            traffic = None
+    traffic, traffic_note = _traffic(tfile, dom, table) if dom else (None, "no tagged launch")
     # network FLOPs per timed step, weighted by the branches actually taken (a cheap-branch
     # image-step runs no network and counts 0): the launches only covered the expensive images
     total_flops = sum(tot_fl.values()) / args.steps
@@ -487,7 +559,7 @@ def main():
                        "parallelism": f"image-shard x{world} (no data-path collective)"},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_note,
                          "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
             "branch_census": {"expensive_image_steps": exp_steps, "image_steps": B * args.steps,
                               "expensive_frac": round(exp_steps / (B * args.steps), 4)},

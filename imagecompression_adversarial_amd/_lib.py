@@ -38,6 +38,7 @@ _SIGS = {
     "ica_conv_up3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
+    "ica_last_launch": [_p, _i, _p],
     "ica_pack_gdn": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_gdn_bf16": [_p, _p, _p, _p, _i, _i, _f, _p],
     "ica_pack_up3_size": [_i],

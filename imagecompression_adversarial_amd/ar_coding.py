@@ -62,7 +62,10 @@ class ArCoder:
         yhat = torch.zeros((B, M, H + 4, W + 4), device=y4.device)
         sym = torch.empty((B, H * W * M), dtype=torch.int32, device=y4.device)
         idx = torch.empty_like(sym)
-        a = self._args(B, H, W, y4=y4.contiguous(), params4=params4.contiguous(), yhat=yhat, sym=sym, idx=idx)
+        # the contiguous copies stay bound to locals while the launch that reads them is enqueued (ArArgs holds raw
+        # pointers only)
+        y4c, p4c = y4.contiguous(), params4.contiguous()
+        a = self._args(B, H, W, y4=y4c, params4=p4c, yhat=yhat, sym=sym, idx=idx)
         call("ica_ar_step", C.c_void_p(C.addressof(a)), 0, H * W, 0, stream())
         return sym, idx, K.to_nc4(yhat[:, :, 2:H + 2, 2:W + 2].contiguous())
 
@@ -79,6 +82,7 @@ class ArCoder:
         sym_in = torch.empty((B, M), dtype=torch.int32, device=dev)
         idx_h = torch.empty((B, M), dtype=torch.int32).pin_memory()
         sym_h = torch.empty((B, M), dtype=torch.int32).pin_memory()
+        p4c = params4.contiguous()   # alive for all H*W+1 step launches that read it through ArArgs
         bufs = [np.frombuffer(s, np.uint8) for s in strings]
         decs = (C.c_void_p * B)()
         v = C.c_void_p
@@ -89,7 +93,7 @@ class ArCoder:
                 if rc != 0:
                     raise RuntimeError(f"context-model bitstream {b} is malformed ({rc})")
                 decs[b] = h
-            a = self._args(B, H, W, params4=params4.contiguous(), yhat=yhat, idx=idx, sym_in=sym_in, means=means)
+            a = self._args(B, H, W, params4=p4c, yhat=yhat, idx=idx, sym_in=sym_in, means=means)
             pa = C.c_void_p(C.addressof(a))
             bad = C.c_int(-1)
             for p in range(H * W + 1):

@@ -772,12 +772,15 @@ class ScaleHyperprior(CompressionModel):
 
 
 def _ar_coder(model):
-    """The model's packed context-model coder (ar_coding.ArCoder), rebuilt when a parameter changes."""
+    """The model's packed context-model coder (ar_coding.ArCoder), rebuilt when a parameter changes or when the
+    GaussianConditional's scale table / bound (buffers, replaced by update_scale_table(force=True)) change: the coder
+    emits indexes into that table."""
     from .ar_coding import ArCoder
-    key = tuple((p.data_ptr(), p._version) for p in model.parameters())
+    gc = model.gaussian_conditional
+    key = (tuple((p.data_ptr(), p._version) for p in model.parameters()),
+           gc.scale_table.data_ptr(), gc.scale_table._version, tuple(gc.scale_table.shape), float(gc.scale_bound))
     cache = getattr(model, "_ar_cache", None)
     if cache is None or cache[0] != key:
-        gc = model.gaussian_conditional
         sd = {k: v.detach() for k, v in model.state_dict().items()}
         cache = (key, ArCoder(sd, model.M, gc.scale_table.to(model.entropy_bottleneck.quantiles.device),
                               float(gc.scale_bound)))

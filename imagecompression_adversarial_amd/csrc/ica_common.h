@@ -150,6 +150,29 @@ inline int ica_cu_count() {
   return cus;
 }
 
+// The conv launchers record the kernel and grid of their last launch (ICA_LAUNCH), so that a host that just timed
+// a tagged launch can ask which kernel that was (ica_last_launch): bench.py checks its PMC traffic stamps with it.
+struct IcaLaunchRec {
+  const void* fn;
+  unsigned long long threads;   // grid x block, as rocprofv3's Grid_Size
+};
+inline IcaLaunchRec& ica_launch_rec() {
+  static thread_local IcaLaunchRec r{nullptr, 0};
+  return r;
+}
+template <typename F>
+inline const void* ica_fnptr(F* f) {   // a kernel (function designator or pointer variable) -> its host stub
+  return reinterpret_cast<const void*>(f);
+}
+#define ICA_LAUNCH(kern, grid, block, lds, st, ...)                                                           \
+  do {                                                                                                       \
+    const dim3 ica_g_ = (grid), ica_b_ = (block);                                                                \
+    ica_launch_rec() = IcaLaunchRec{ica_fnptr(kern),                                                        \
+                                    (unsigned long long)ica_g_.x * ica_g_.y * ica_g_.z * ica_b_.x * ica_b_.y * \
+                                        ica_b_.z};                                                           \
+    hipLaunchKernelGGL(kern, ica_g_, ica_b_, lds, st, __VA_ARGS__);                                          \
+  } while (0)
+
 #define ICA_CHECK_LAUNCH()                          \
   do {                                              \
     hipError_t _e = hipGetLastError();              \

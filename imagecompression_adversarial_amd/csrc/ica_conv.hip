@@ -20,7 +20,11 @@
 //               parity classes (9/6/6/4 taps).  Block = 8x32 output pixels
 //               (4x16 per class); the whole-Cin input patch lives in LDS; each
 //               wave runs two class tiles paired 9+4 / 6+6 for balance.
+#include <cxxabi.h>
+
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ica_conv_epi.h"
@@ -1244,8 +1248,8 @@ gather:
 // conv_up3 on x6 operands, persistent and pipelined (the default for Cin = 128 / 192).  A tile is R = 4 CT - 2 input
 // rows x 30 columns; its Z = W^T x (75 x Cin, fp32-accurate bf16x6 MFMAs) covers the (R + 2) x 32 halo, i.e. exactly
 // one 32-pixel MFMA column tile per halo row, CT rows per wave (Z in LDS: 75 x 4 CT x 32 floats; the halo costs
-// (R + 2) x 32 / (R x 30) = 1.28x at CT = 3 instead of the 5 x 32 tile's 1.49x).  Each block walks a contiguous run of
-// tiles; the activations of tile t+1 are loaded into the registers of tile t's as each chunk is consumed (one whole
+// (R + 2) x 32 / (R x 30) = 1.28x at CT = 3 instead of the 5 x 32 tile's 1.49x).  Each block walks its tiles (see the
+// tile order below); the activations of its next tile are loaded into the registers of the current one's as each chunk is consumed (one whole
 // tile of prefetch distance, no extra registers), so the kernel streams instead of waiting out one HBM round trip per
 // chunk (the 5 x 32 kernel ran 8 dependent chunk loads per tile: latency-bound at 0.17 of the x6 ceiling).
 // Weights: the pack_up3_x6 fragments, one chunk's 9 fragments a chunk ahead, shared by the CT column tiles.
@@ -1257,15 +1261,21 @@ template <int CT>
 constexpr int u3_npx() { return 4 * CT * U3_HW; }
 
 template <int NCH, int CT>
-__global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int tiles_per_block) {
+__global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p) {
   constexpr int R = u3_rows<CT>(), NPX = u3_npx<CT>();
   __shared__ float zs[T3_ROWS * NPX];
   const int tiles_x = (p.Win + U3_OW - 1) / U3_OW, tiles_y = (p.Hin + R - 1) / R;
   const int total = tiles_x * tiles_y * p.N;
-  int blk, by;
-  xcd_block<true>(blk, by);
-  (void)by;
-  const int t_begin = blk * tiles_per_block, t_end = min(total, t_begin + tiles_per_block);
+  // Tile order (speed only; every tile runs the same instructions whichever block takes it): the grid is 8 x nb
+  // blocks, dealt round-robin over the XCDs, so block b runs on XCD b % 8.  XCD x owns one contiguous eighth of the
+  // tiles and its nb blocks take them interleaved (block i: tiles i, i + nb, ...), so at any moment an XCD's blocks
+  // work on ~nb NEIGHBOURING tiles: the halo lines two tiles share are fetched from HBM once and hit in that XCD's
+  // L2 for the other.  (Contiguous runs per block put concurrent tiles ~40 tiles apart: every shared line came from
+  // HBM twice, and the 30-column tiles' misaligned 256-B runs cost 1.79x the input bytes.)
+  const int nb = (int)(gridDim.x >> 3), xcd = (int)(blockIdx.x & 7), bi = (int)(blockIdx.x >> 3);
+  const int q8 = total >> 3, r8 = total & 7;
+  const int t_end = xcd * q8 + min(xcd, r8) + q8 + (xcd < r8 ? 1 : 0);
+  const int t_begin = xcd * q8 + min(xcd, r8) + bi;
   if (t_begin >= t_end) return;   // block-uniform
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1327,10 +1337,10 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p, int 
   };
   const float bias0 = p.bias ? p.bias[0] : 0.f, bias1 = p.bias ? p.bias[1] : 0.f, bias2 = p.bias ? p.bias[2] : 0.f;
 #pragma unroll 1
-  for (int t = t_begin; t < t_end; ++t) {
+  for (int t = t_begin; t < t_end; t += nb) {
     wz = 0;
     asm volatile("" : "+s"(wz));
-    prep(t + 1, t + 1 < t_end, rn, vbn);
+    prep(t + nb, t + nb < t_end, rn, vbn);
     f32x16 acc[CT][3];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
@@ -1579,7 +1589,7 @@ static int launch_down(const ConvParams& p, hipStream_t st) {
   constexpr int TH = down_pt<CC, BF>() * 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  hipLaunchKernelGGL((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O>), grid, dim3(256), 0, st, p);
+  ICA_LAUNCH((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1638,7 +1648,7 @@ template <int KS, int S, int IT, int EPI, int FX>
 static int launch_down_split(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Wout + DS_TW - 1) / DS_TW) * ((p.Hout + DS_TH - 1) / DS_TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  hipLaunchKernelGGL((conv_down_split_kernel<KS, S, IT, EPI, FX>), grid, dim3(256), 0, st, p);
+  ICA_LAUNCH((conv_down_split_kernel<KS, S, IT, EPI, FX>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1750,7 +1760,7 @@ static int launch_up_small(const ConvParams& p, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_small_kernel<KS, IT, EPI, FX>), grid, dim3(256), lds, st, p);
+  ICA_LAUNCH((conv_up_small_kernel<KS, IT, EPI, FX>), grid, dim3(256), lds, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1775,7 +1785,7 @@ static int launch_up(const ConvParams& p, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_kernel<KS, IT, EPI, FX, BF>), grid, dim3(256), lds, st, p);
+  ICA_LAUNCH((conv_up_kernel<KS, IT, EPI, FX, BF>), grid, dim3(256), lds, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1856,6 +1866,21 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
 
 // C-ABI argument block of ica_conv_ex (mirrors include/ica_hip.h)
 extern "C" {
+int ica_last_launch(char* name, int cap, unsigned long long* threads) {
+  const IcaLaunchRec r = ica_launch_rec();
+  if (!r.fn) return -1;
+  if (threads) *threads = r.threads;
+  if (name && cap > 0) {
+    const char* m = hipKernelNameRefByPtr(r.fn, nullptr);
+    int st = -1;
+    char* d = m ? abi::__cxa_demangle(m, nullptr, nullptr, &st) : nullptr;
+    const char* src = (st == 0 && d) ? d : (m ? m : "");
+    std::snprintf(name, (size_t)cap, "%s", src);
+    std::free(d);
+  }
+  return 0;
+}
+
 typedef struct ica_conv_args {
   const float* x;
   float* y;
@@ -1898,7 +1923,7 @@ int ica_pack_conv_weight(const float* w, float* dst, int O, int C, int KS, long 
                          int flip, int it, hipStream_t st) {
   const int IT = resolve_it(O, it);
   const long total = (long)ica_pack_conv_weight_size(O, C, KS, CC, IT);
-  hipLaunchKernelGGL(pack_conv_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc,
+  ICA_LAUNCH(pack_conv_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, O, C, KS, so, sc,
                      IT, CC, order, total, flip);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -1944,13 +1969,13 @@ int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, l
   if (C <= 4) {  // conv_down tap groups (RGB input)
     if (order != 0) return -4;
     const long tot = (long)ica_pack_conv_weight_bf16_size(O, C, KS, IT);
-    hipLaunchKernelGGL(pack_conv_tg_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
+    ICA_LAUNCH(pack_conv_tg_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
                        O, C, KS, so, sc, IT, tot, flip);
     ICA_CHECK_LAUNCH();
     return 0;
   }
   const long total = (long)ica_pack_conv_weight_size(O, C, KS, 16, IT);
-  hipLaunchKernelGGL(pack_conv_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
+  ICA_LAUNCH(pack_conv_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, IT, 16, order, total, flip);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -1963,7 +1988,7 @@ size_t ica_pack_up3_size(int Cin) { return (size_t)3 * (Cin / 16) * 64 * 8; }
 int ica_pack_up3(const float* w, float* dst, int Cin, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
   const long total = (long)ica_pack_up3_size(Cin);
-  hipLaunchKernelGGL(pack_up3_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, Cin, total);
+  ICA_LAUNCH(pack_up3_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, w, dst, Cin, total);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1983,7 +2008,7 @@ int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, i
                2 * Hin, 2 * Win, nullptr};
   p.pl = layout;
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
-  hipLaunchKernelGGL(conv_up3_kernel<false>, dim3(tiles), dim3(256), 0, st, p);
+  ICA_LAUNCH(conv_up3_kernel<false>, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1993,7 +2018,7 @@ int ica_conv_up3(const float* x, float* y, const float* wp, const float* bias, i
 int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
   const long total = (long)ica_pack_up3_size(Cin);
-  hipLaunchKernelGGL(pack_up3_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
+  ICA_LAUNCH(pack_up3_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), Cin, total);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -2006,11 +2031,10 @@ int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias,
   ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
   p.pl = layout;
-  auto persistent = [&](auto kern, int R) {
+  auto persistent = [&](auto kern, int R) {   // 8 x nb blocks: nb per XCD, at most one per CU
     const int tiles = ((Win + U3_OW - 1) / U3_OW) * ((Hin + R - 1) / R) * N;
-    const int nblk = std::max(1, std::min(tiles, ica_cu_count()));
-    const int per = (tiles + nblk - 1) / nblk;
-    hipLaunchKernelGGL(kern, dim3((tiles + per - 1) / per), dim3(256), 0, st, p, per);
+    const int nb = std::max(1, std::min((tiles + 7) / 8, ica_cu_count() / 8));
+    ICA_LAUNCH(kern, dim3(8 * nb), dim3(256), 0, st, p);
   };
   if (Cin == 128) {
     persistent(conv_up3_x6p_kernel<8, 3>, u3_rows<3>());
@@ -2018,7 +2042,7 @@ int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias,
     persistent(conv_up3_x6p_kernel<12, 2>, u3_rows<2>());
   } else {
     const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
-    hipLaunchKernelGGL((conv_up3_kernel<false, true>), dim3(tiles), dim3(256), 0, st, p);
+    ICA_LAUNCH((conv_up3_kernel<false, true>), dim3(tiles), dim3(256), 0, st, p);
   }
   ICA_CHECK_LAUNCH();
   return 0;
@@ -2028,7 +2052,7 @@ int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias,
 int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t st) {
   if (Cin % 16 != 0) return -2;
   const long total = (long)ica_pack_up3_size(Cin);
-  hipLaunchKernelGGL(pack_up3_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
+  ICA_LAUNCH(pack_up3_kernel<__bf16>, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), Cin, total);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -2042,7 +2066,7 @@ int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bia
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
   p.pl = layout;
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
-  hipLaunchKernelGGL(conv_up3_kernel<true>, dim3(tiles), dim3(256), 0, st, p);
+  ICA_LAUNCH(conv_up3_kernel<true>, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -2086,7 +2110,7 @@ int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* b
                       float beta_bound, hipStream_t st) {
   if (C % 32 != 0) return -2;
   const long total = (long)(C / 32) * (C / 32) * 2048;
-  hipLaunchKernelGGL(pack_gdn_bf16_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gamma, beta,
+  ICA_LAUNCH(pack_gdn_bf16_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gamma, beta,
                      reinterpret_cast<__bf16*>(gpb), beta_eff, C, transpose, beta_bound);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -2096,7 +2120,7 @@ int ica_pack_gdn(const float* gamma, const float* beta, float* gp, float* beta_e
                  float beta_bound, hipStream_t st) {
   if (C % 32 != 0) return -2;
   const long total = (long)(C / 32) * (C / 32) * 64 * 16;
-  hipLaunchKernelGGL(pack_gdn_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gamma, beta, gp, beta_eff, C,
+  ICA_LAUNCH(pack_gdn_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gamma, beta, gp, beta_eff, C,
                      transpose, beta_bound);
   ICA_CHECK_LAUNCH();
   return 0;

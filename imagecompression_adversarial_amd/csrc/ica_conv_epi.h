@@ -929,3 +929,80 @@ ICA_DEV void gdn_bwd_x6_wide(const ConvParams& p, f32x16 (&acc)[IT], int n, int 
       }
   }
 }
+
+// --------------------------------------------------------------------------
+// x6 GDN / IGDN forward epilogue for kernels at TWO waves per SIMD (256 registers; conv_up_x6w): the two pixel
+// tiles' 128 accumulator registers are live on entry, so the pair form's 2 x IT normaliser tiles do not fit.  One
+// tile at a time (the other tile's 64 registers wait), one normaliser tile ct at a time (x^2 split per round, the
+// gamma' fragments of round k+1 issued before round k's MFMAs): the arithmetic, MFMA order and bits of
+// gdn_fwd_x6_pair.  (A GDN-backward counterpart at 256 registers -- t kept or split, g*s parked in the output, u
+// per output tile -- measured 17-20 % slower than the 4-wave kernel's wide epilogue and is not built.)
+// --------------------------------------------------------------------------
+template <int IT, int EPI>
+ICA_DEV void gdn_fwd_x6_tile_narrow(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox) {
+  static_assert(EPI == EPI_GDN || EPI == EPI_IGDN, "forward GDN epilogues only");
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+  const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout), ers = chan_rsrc(p.beta, p.Cout);
+  const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = ld_chan4(brs, it * 32 + 8 * g + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += bv[e];
+    }
+  }
+  auto ldg = [&](bf16x8 (&a)[3], int ct, int k) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      a[q] = ld_bf8(grs, lane * 16, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+  };
+  const bool ok = oy < p.Hout && ox < p.Wout;
+  const unsigned vo = h * plane + (ok ? pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u);
+#pragma unroll
+  for (int ct = 0; ct < IT; ++ct) {
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 nx;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) nx[4 * g + e] = ev[e];
+    }
+    bf16x8 ga[2][3];
+    ldg(ga[0], ct, 0);
+#pragma unroll
+    for (int k = 0; k < 2 * IT; ++k) {
+      if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], ct, k + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = acc[k >> 1][8 * (k & 1) + j] * acc[k >> 1][8 * (k & 1) + j];
+      bf16x8 xq[3];
+      split3x8(v, xq);
+      nx = mfma_x6(ga[k & 1], xq, nx);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (ok) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 yv, sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float nv = nx[4 * g + e];
+          const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+          sv[e] = sc;
+          yv[e] = acc[ct][4 * g + e] * sc;
+        }
+        const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
+        if (p.save_s) SS.st(vo, ss, sv);
+        Y.st(vo, ss, yv);
+      }
+    }
+  }
+}

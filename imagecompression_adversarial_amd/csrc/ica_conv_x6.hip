@@ -532,6 +532,160 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
 }
 
 // --------------------------------------------------------------------------------------------------------------
+// conv_up_x6w: the conv_up_x6 block (8 x 16 input pixels, the channel group in LDS) on EIGHT waves, one output-parity
+// class per wave, two waves per SIMD (waves w and w + 4 share one).  The partners run complementary classes (9 + 4 or
+// 6 + 6 taps), so while one wave is in its epilogue (saved (y, s) reads, VALU, stores) or waits on a load, the
+// other's MFMAs keep the SIMD's matrix pipe busy; at one wave per SIMD (conv_up_x6) every epilogue and wait left it
+// idle.  256 registers per wave: the weight fragments of output tile it are refilled right after that tile's MFMAs
+// of the step (a ring, one step of prefetch distance, instead of two whole fragment sets), one B operand set, and the
+// GDN forward epilogue is the tile-serial narrow form.  Each output runs the same MFMA and epilogue arithmetic as in
+// conv_up_x6: same bits (scripts/gpu_ab_bits.sh).  Forward layers only (launch_up_x6): bias 2.98 -> 2.73 ms, IGDN
+// 3.66 -> 3.44 ms at the config-2 shapes (row-major, same box).
+// --------------------------------------------------------------------------------------------------------------
+template <int PY, int PX, int IT, int CG>
+ICA_DEV void conv_up_x6w_class(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch, int grp, long ps,
+                               f32x16 (&acc)[2][IT]) {
+  constexpr int PT = 2, KS = 5, PAD = 2, XU_PLANE = xu_plane<PT>();
+  constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
+  constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
+  constexpr int NCG = CG / 16;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * KS * KS * nch * IT * 64;
+  const int total = NT * NCG;
+  auto ldw = [&](bf16x8 (&a)[3], int u, int it) {   // output tile it's fragments of step u
+    u = min(u, total - 1);
+    const int ti = u / NCG, c = u - ti * NCG;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int f = wbase + ((ky * KS + kx) * nch + grp * NCG + c) * IT * 64 + it * 64;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] = ld_bf8(wr, lane * 16, (int)((q * ps + f) * 16));
+  };
+  auto ldb = [&](bf16x8 (&b)[PT][3], int u) {
+    u = min(u, total - 1);
+    const int ti = u / NCG, c = u - ti * NCG;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int pr = a_rel + 1 + (PY + PAD - ky) / 2, pc = b_rel + 1 + (PX + PAD - kx) / 2;
+    const int e = (2 * c + h) * XU_PLANE + pr * XU_PC + pc;
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int o = e + t * 2 * XU_PC;
+      b[t][0] = f4_as_bf8(patch[o]);
+      b[t][1] = f4_as_bf8(patch[(CG / 8) * XU_PLANE + o]);
+      b[t][2] = f4_as_bf8(patch[2 * (CG / 8) * XU_PLANE + o]);
+    }
+  };
+  // one B set: the next step's LDS operands are read after this step's last MFMA (the SIMD partner's MFMAs cover
+  // their latency)
+  bf16x8 w[IT][3], b[PT][3];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) ldw(w[it], 0, it);
+  ldb(b, 0);
+#pragma unroll 1
+  for (int u = 0; u < total; ++u) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) acc[t][it] = mfma_x6(w[it], b[t], acc[t][it]);
+      ldw(w[it], u + 1, it);   // after this step's last use: one step ahead of the next
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    ldb(b, u + 1);
+  }
+}
+
+template <int IT, int EPI, int CG>
+__global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long ps) {
+  constexpr int PT = 2, NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
+  extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
+  const int tiles_x = (p.Win + XU_TW - 1) / XU_TW, tiles_y = (p.Hin + XU_TH - 1) / XU_TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int a0 = ty * XU_TH, b0 = tx * XU_TW;
+  const int Cin4 = p.Cin >> 2, nch = p.Cin / 16, ngrp = p.Cin / CG;
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  auto fill = [&](int grp) __attribute__((always_inline)) {
+    constexpr int FB = 6, TOT = NQ * XU_PLANE;
+    __syncthreads();
+    for (int e0 = threadIdx.x; e0 < TOT; e0 += 512 * FB) {
+      f32x4 v[FB];
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        const int e = e0 + 512 * i;
+        const int q = e / XU_PLANE, rem = e - q * XU_PLANE, pr = rem / XU_PC, pc = rem - pr * XU_PC;
+        const int iy = a0 - 1 + pr, ix = b0 - 1 + pc;
+        const bool ok = e < TOT && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+        const unsigned vo = ((unsigned)(grp * NQ + q) * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        const int e = e0 + 512 * i;
+        if (e < TOT) {
+          const int q = e / XU_PLANE, pix = e - q * XU_PLANE;
+          u32x2 a, b, c;
+          split3(v[i], a, b, c);
+          const int ent = (q >> 1) * XU_PLANE + pix;
+          p2[(0 * (CG / 8) * XU_PLANE + ent) * 2 + (q & 1)] = a;
+          p2[(1 * (CG / 8) * XU_PLANE + ent) * 2 + (q & 1)] = b;
+          p2[(2 * (CG / 8) * XU_PLANE + ent) * 2 + (q & 1)] = c;
+        }
+      }
+    }
+    __syncthreads();
+  };
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int jt = wave & 1;
+  const int j = threadIdx.x & 31;
+  const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
+  auto run_class = [&](auto py_c, auto px_c, bool refill) __attribute__((always_inline)) {
+    constexpr int PY = decltype(py_c)::value, PX = decltype(px_c)::value;
+    f32x16 acc[PT][IT];
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
+    for (int grp = 0; grp < ngrp; ++grp) {
+      if (refill) fill(grp);
+      conv_up_x6w_class<PY, PX, IT, CG>(p, patch, jt, cb, nch, grp, ps, acc);
+    }
+    const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
+    const int ox[2] = {2 * (b0 + b_rel) + PX, 2 * (b0 + b_rel) + PX};
+    static_assert(EPI == EPI_BIAS || EPI == EPI_GDN || EPI == EPI_IGDN, "conv_up_x6w: forward epilogues");
+    if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
+#pragma unroll
+      for (int t = 0; t < PT; ++t) gdn_fwd_x6_tile_narrow<IT, EPI>(p, acc[t], n, oy[t], ox[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < PT; ++t)
+        conv_epilogue<IT, EPI, 0, false, 2>(p, acc[t], n, oy[t], ox[t], oy[t] < p.Hout && ox[t] < p.Wout,
+                                            cb * IT * 32);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  const bool multi = ngrp > 1;
+  if (!multi) fill(0);
+  // SIMD partners (w, w + 4): (0,0) 9 taps with (1,1) 4 taps; (0,1) with (1,0), 6 + 6.  Every wave joins every
+  // fill barrier (one class each, the same group sequence)
+  switch (wave >> 1) {
+    case 0: run_class(I0{}, I0{}, multi); break;
+    case 1: run_class(I0{}, I1{}, multi); break;
+    case 2: run_class(I1{}, I1{}, multi); break;
+    default: run_class(I1{}, I0{}, multi); break;
+  }
+}
+
+// --------------------------------------------------------------------------------------------------------------
 // Small-grid x6 kernels (layers whose low-resolution side is <= 32 x 32 per image: the fine-tune's 256x256 crops).
 // The structure of the fp32 small-grid kernels of ica_conv.hip on x6 operands: a 32-pixel tile per
 // block, the K loop split over the 4 waves, partial sums reduced through LDS in wave order (deterministic), wave 0
@@ -833,7 +987,7 @@ int launch_down_x6_pt(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + xd_th<PT>() - 1) / xd_th<PT>()) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * ((((p.Cin + 3) / 4) * 4 + 15) / 16) * 25 * IT * 64;
-  hipLaunchKernelGGL((conv_down_x6_kernel<IT, EPI, PT>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+  ICA_LAUNCH((conv_down_x6_kernel<IT, EPI, PT>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -845,7 +999,7 @@ int launch_down_small_x6(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Wout + XSD_TW - 1) / XSD_TW) * ((p.Hout + XSD_TH - 1) / XSD_TH) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * ((((p.Cin + 3) / 4) * 4 + 15) / 16) * 25 * IT * 64;
-  hipLaunchKernelGGL((conv_down_small_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+  ICA_LAUNCH((conv_down_small_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -872,10 +1026,10 @@ int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
     // one block per CU, a contiguous run of tiles each (the XCD-aware order keeps a run's halo rows in one L2)
     const int nblk = std::max(1, std::min(tiles, ica_cu_count() / ncb));
     const int per = (tiles + nblk - 1) / nblk;
-    hipLaunchKernelGGL((conv_rgb_bwd_x6_kernel<IT, EPI>), dim3((tiles + per - 1) / per, ncb), dim3(256), 0, st, p, ps,
+    ICA_LAUNCH((conv_rgb_bwd_x6_kernel<IT, EPI>), dim3((tiles + per - 1) / per, ncb), dim3(256), 0, st, p, ps,
                        per);
   } else {
-    hipLaunchKernelGGL((conv_rgb_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+    ICA_LAUNCH((conv_rgb_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
   }
   ICA_CHECK_LAUNCH();
   return 0;
@@ -894,7 +1048,24 @@ int launch_up_x6_pt(const ConvParams& p, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_x6_kernel<IT, EPI, CG, PT>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_LAUNCH((conv_up_x6_kernel<IT, EPI, CG, PT>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int IT, int EPI, int CG>
+int launch_up_x6w(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * 25 * (p.Cin / 16) * IT * 64;
+  constexpr size_t lds = xu_lds_bytes<CG, 2>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6w_kernel<IT, EPI, CG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  ICA_LAUNCH((conv_up_x6w_kernel<IT, EPI, CG>), dim3(tiles, ncb), dim3(512), lds, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -913,6 +1084,9 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
   const long b2 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N * ncb;
   const long b1 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<1>() - 1) / xu_th<1>()) * p.N * ncb;
   if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) return launch_up_x6_pt<IT, EPI, CG, 1>(p, st);
+  // forward layers (bias / IGDN): the 8-wave class-per-wave kernel; the GDN backward keeps the 4-wave kernel, whose
+  // wide epilogue needs the whole register file (its two-tile narrow form at 256 registers measured 17 % slower)
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_IGDN || EPI == EPI_GDN) return launch_up_x6w<IT, EPI, CG>(p, st);
   return launch_up_x6_pt<IT, EPI, CG, X6_PT>(p, st);
 }
 
@@ -929,7 +1103,7 @@ int launch_up_small_x6(const ConvParams& p, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_up_small_x6_kernel<IT, EPI>), dim3(4 * tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_LAUNCH((conv_up_small_x6_kernel<IT, EPI>), dim3(4 * tiles, ncb), dim3(256), lds, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1007,7 +1181,7 @@ size_t ica_pack_gdn_x6_size(int C) { return (size_t)3 * (C / 32) * (C / 32) * 20
 int ica_pack_gdn_x6(const float* gp, void* dst, int C, hipStream_t st) {
   if (C % 32 != 0) return -2;
   const long total = (long)(C / 32) * (C / 32) * 1024;
-  hipLaunchKernelGGL(pack_gdn_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gp,
+  ICA_LAUNCH(pack_gdn_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, gp,
                      reinterpret_cast<__bf16*>(dst), total);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -1019,7 +1193,7 @@ int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, lon
                             hipStream_t st) {
   if (it <= 0) return -3;
   const long total = (long)ica_pack_conv_weight_x6_size(O, C, KS, it) / 3;
-  hipLaunchKernelGGL(pack_conv_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
+  ICA_LAUNCH(pack_conv_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, it, order, total);
   ICA_CHECK_LAUNCH();
   return 0;

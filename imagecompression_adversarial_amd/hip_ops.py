@@ -42,6 +42,38 @@ def _ev_end(h, flops=None):
         EVENT_HOOK.setdefault(h[0], []).append((h[1], e1, h[2]))
         if flops is not None:
             FLOPS_HOOK[h[0]] = flops / max(h[2], 1)
+        if LAUNCH_HOOK is not None:
+            LAUNCH_HOOK.setdefault(h[0], set()).add(last_launch())
+
+
+# kernels behind each tagged launch (filled while EVENT_HOOK and LAUNCH_HOOK are set): {tag: {(kernel, threads)}}
+LAUNCH_HOOK = None
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the HIP sources the library is built from (csrc/*.hip, *.h, in name order):
+    the revision stamp of a PMC traffic measurement."""
+    import glob
+    import hashlib
+    import os
+    h = hashlib.sha256()
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    for f in sorted(glob.glob(os.path.join(d, "*.hip")) + glob.glob(os.path.join(d, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def last_launch():
+    """(demangled kernel name, grid size in threads) of this thread's last conv launch (ica_last_launch): the names
+    and Grid_Size that rocprofv3 reports for the same dispatch."""
+    import ctypes as C
+    buf = C.create_string_buffer(512)
+    thr = C.c_ulonglong(0)
+    if lib().ica_last_launch(buf, 512, C.byref(thr)) != 0:
+        return None
+    return buf.value.decode(errors="replace"), int(thr.value)
 
 
 # operand precision of each tagged conv launch (filled while EVENT_HOOK is set): what actually ran, small-grid

@@ -1,15 +1,27 @@
 """Per-kernel timing of the k5 s2 conv launches on the bench shapes (hyper q3, 512x768, B=32), fp32-MFMA vs the
 fp32-accurate bf16x6 kernels.  Interleaved rounds in one process; median ms and TFLOP/s.
-    python scripts/kbench_x6.py [B] [--only substring]"""
+    python scripts/kbench_x6.py [B] [--only substring] [--dump out.pt]
+--dump saves every case's output (one more call) so that two libraries (ICA_HIP_LIB) can be compared bit for bit:
+    python scripts/kbench_x6.py --cmp a.pt b.pt"""
 import statistics
 import sys
 
 import torch
 
+if "--cmp" in sys.argv:
+    a, b = (torch.load(f, weights_only=True) for f in sys.argv[sys.argv.index("--cmp") + 1:][:2])
+    bad = 0
+    for k in a:
+        if k in b:
+            same = torch.equal(a[k], b[k])
+            bad += not same
+            print(f"{k:22s} {'identical' if same else 'DIFFERENT max|d|=%.3g' % float((a[k] - b[k]).abs().max())}")
+    sys.exit(1 if bad else 0)
 sys.path.insert(0, ".")
 from imagecompression_adversarial_amd import hip_ops as K  # noqa: E402
 
 dev = torch.device("cuda:0")
+torch.manual_seed(0)   # the activation / saved-tensor inputs come from the default generator: same bits per process
 B = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 32
 only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else ""
 N = 128
@@ -74,3 +86,10 @@ for k, v in times.items():
     ms = statistics.median(v)
     fl = flop_rgb if ("rgb" in k or "up3" in k) else flop
     print(f"{k:22s} {ms:7.3f} ms  {fl / ms / 1e9:7.1f} TFLOP/s (conv only)", flush=True)
+if "--dump" in sys.argv:
+    res = {}
+    for k, f in cases.items():
+        o = f()
+        o = [t for t in o if isinstance(t, torch.Tensor)] if isinstance(o, tuple) else [o]
+        res[k] = torch.cat([t.float().reshape(-1).cpu() for t in o])
+    torch.save(res, sys.argv[sys.argv.index("--dump") + 1])

@@ -1,6 +1,6 @@
 """Per-kernel register / spill / LDS table of one HIP source (hipcc -Rpass-analysis=kernel-resource-usage).
 
-usage: python scripts/kres.py imagecompression_adversarial_amd/csrc/ica_conv_x6.hip [name-filter]
+usage: python scripts/kres.py imagecompression_adversarial_amd/csrc/ica_conv_x6.hip [name-filter] [-Dflags...]
 """
 import os
 import re
@@ -12,7 +12,7 @@ def main():
     src = os.path.abspath(sys.argv[1])
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
     out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", src,
-                          "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"],
+                          "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[3:],
                          capture_output=True, text=True, cwd="/tmp").stderr
     rows, cur = [], None
     for line in out.splitlines():
