@@ -49,6 +49,10 @@ TAGS = ("t100a", "t100b")
 NOISE_MAX, NOISE_P999 = 6e-2, 1.8e-2
 # first step whose branch differs from the reference's (100 = none), as achieved on MI355X by each path
 DIV_MIN = {("t100a", "fp32"): 100, ("t100b", "fp32"): 100, ("t100a", "x6"): 100, ("t100b", "x6"): 100}
+# the HIP paths' own p99.9 bound, ~2-3x the largest p99.9 each path measured on MI355X over the snapshot steps and
+# the final noise (rounds 3-4: t100a fp32 3.0e-5, x6 8.3e-5; t100b fp32 4.4e-4, x6 2.3e-3): the calibrated CPU
+# bound NOISE_P999 above is ~10x looser than any path needs, so a several-fold loss of accuracy would pass it
+P999_PATH = {("t100a", "fp32"): 1e-4, ("t100a", "x6"): 2e-4, ("t100b", "fp32"): 1e-3, ("t100b", "x6"): 5e-3}
 
 
 @pytest.fixture(scope="module")
@@ -176,14 +180,14 @@ def test_hip_traj100_vs_reference(t100, tag, precision):
         if i < div:
             mx, p999 = _noise_close(snaps[i], snap[f"{tag}_snap"][k])
             print(f"{tag}/{precision}: noise after step {i}: rel diff max {mx:.2e}, p99.9 {p999:.2e}")
-            assert mx <= NOISE_MAX and p999 <= NOISE_P999, (i, mx, p999)
+            assert mx <= NOISE_MAX and p999 <= min(NOISE_P999, P999_PATH[(tag, precision)]), (i, mx, p999)
     if div == 100:
         # Adam's 1/sqrt(v) amplifies fp32 ordering differences where |g| ~ eps (NOISE_MAX / NOISE_P999 above; for
         # scale: the SAME algorithm in fp64 leaves the fp32 reference's branch sequence at step 32 (t100a) / 40
         # (t100b) and ends O(1) away, max 1.3 / 1.5, p99.9 0.95 / 0.99 of max|noise|)
         mx, p999 = _noise_close(loop.noise.cpu().numpy(), t100[f"{tag}_noise"])
         print(f"{tag}/{precision}: final noise rel diff max {mx:.2e}, p99.9 {p999:.2e}")
-        assert mx <= NOISE_MAX and p999 <= NOISE_P999, (mx, p999)
+        assert mx <= NOISE_MAX and p999 <= min(NOISE_P999, P999_PATH[(tag, precision)]), (mx, p999)
     res = evaluate(kern, loop.im_in, loop.im_s, loop.output_s, msssim=False)
     mse_in, mse_out = float(res[3][0]), float(res[4][0])
     assert abs(mse_in - float(t100[f"{tag}_mse_in"])) <= 0.1 * float(t100[f"{tag}_mse_in"])
