@@ -170,6 +170,373 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
 }
 
 // --------------------------------------------------------------------------------------------------------------
+// conv_down_x6w: the k5 s2 conv of 128 output channels (IT = 4) on EIGHT waves, two per SIMD.  Block = 4 PT x 32
+// output pixels (as conv_down_x6); wave w owns output rows PT (w & 3) .. + PT - 1 and output channels
+// 64 (w >> 2) .. + 63, so the SIMD partners w, w + 4 share the pixels and split the channels.
+//   * K order: 8-channel chunks x tap PAIRS: a 16-deep MFMA k step is channels 8 c .. 8 c + 7 of taps 2 s (lane
+//     half h = 0) and 2 s + 1 (h = 1).  Chunks run in pairs whose two taps 24 form one cross step (lane half h =
+//     chunk 2 cp + h), so a pair of 8-channel chunks is 25 steps, as many as one 16-channel chunk x 25 taps.
+//   * An 8-channel patch is 61 KB (three bf16 planes), so two fit in LDS: the next chunk's loads are issued at the
+//     start of a chunk's 12 steps and split into the other buffer in the middle of them (waves 0-3 after step 3,
+//     waves 4-7 after step 8, so the partners' VALU never coincide); three barriers per chunk pair (the cross step
+//     reads both buffers).  At one wave per SIMD the 16-channel patch (122 KB, single buffer) was refilled between
+//     two barriers, ~11 % of conv_down_x6's time.
+//   Measured (kbench_x6, same box): bias 2.82 -> 2.59 ms, GDN 2.92 -> 2.73, IGDN backward 2.94 -> 2.80.  Without
+//   the cross step (13 steps per chunk, tap 25 a zero weight: +4 % MFMAs) the same kernel only matched
+//   conv_down_x6: its MFMA-busy fraction rose 0.67 -> 0.72-0.76 but the chip held a lower clock.
+//   * Patch rows hold their even columns, then their odd ones: the stride-2 pixel reads of 32 lanes are 32
+//     consecutive 16-B entries (conflict-free ds_read_b128).
+//   * Epilogues: after the last chunk the whole LDS is free; each wave publishes what its partner's channels need
+//     (GDN: x = conv + bias; IGDN backward: t) and reads the partner's, so the GDN GEMMs over all 128 channels run
+//     with the arithmetic, MFMA order and bits of the single-wave epilogues (gdn_fwd_x6_pair / the wide backward).
+// Weights: the tap-pair pack that ica_pack_conv_weight_x6 appends to the order-0 pack for KS = 5, IT = 4:
+// [plane][cb][chunk8][step][it][lane] bf16x8, plane stride ps2 fragments, starting 3 ps fragments in.
+// --------------------------------------------------------------------------------------------------------------
+constexpr int XW_NS = 13;   // tap pairs per 8-channel chunk
+__device__ __forceinline__ int xw_pos(int pr, int pc) {   // LDS entry of patch pixel (pr, pc): even columns first
+  constexpr int PC = 2 * 31 + 5, PCE = (PC + 1) / 2;
+  return pr * PC + ((pc & 1) ? PCE + (pc >> 1) : (pc >> 1));
+}
+// PT = 2: 8 x 32 output pixels per block, two rows per wave; PT = 1 (4 x 32, one row per wave) where the PT = 2 grid
+// leaves CUs idle.  Both run the same MFMA and epilogue sequence per output (same bits at any batch size).
+
+template <int EPI, int PT>
+__global__ __launch_bounds__(512, 1) void conv_down_x6w_kernel(ConvParams p, long ps2) {
+  constexpr int IT = 4, ITW = 2, KS = 5, S = 2, PAD = 2, TW = 32, TH = 4 * PT, NS = XW_NS;
+  constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;   // 19 x 67
+  constexpr int PCE = (PC + 1) / 2;
+  constexpr int NF = (2 * PLANE + 511) / 512;                                       // fill entries per thread
+  constexpr int BUF = 3 * PLANE;                                                    // entries per buffer
+  constexpr int XCH = 8 * PT * ITW * 4 * 64;                                        // epilogue exchange entries
+  __shared__ f32x4 lds[(2 * BUF > XCH) ? 2 * BUF : XCH];
+  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
+  int bid, cb;
+  xcd_block<true>(bid, cb);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rp = wave & 3, chh = wave >> 2;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  const int Cin4 = (p.Cin + 3) >> 2, nch = (Cin4 + 1) >> 1;   // 8-channel chunks
+  const unsigned xplane = (unsigned)p.Hin * p.Win;
+  const __amdgpu_buffer_rsrc_t xr =
+      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+  u32x2* l2 = reinterpret_cast<u32x2*>(lds);
+  // fill: entry e = (quad q of the chunk, patch pixel); padding and quads past Cin read out of range (zeros)
+  auto fill_load = [&](int ch, f32x4 (&v)[NF]) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      const int q = e >= PLANE ? 1 : 0, pix = e - q * PLANE, pr = pix / PC, pc = pix - pr * PC;
+      const int iy = iy0 + pr, ix = ix0 + pc, c4 = 2 * ch + q;
+      const bool ok = e < 2 * PLANE && c4 < Cin4 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const unsigned vo = ((unsigned)c4 * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+    }
+  };
+  auto fill_put = [&](int buf, const f32x4 (&v)[NF]) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 512 * i;
+      if (e < 2 * PLANE) {
+        const int q = e >= PLANE ? 1 : 0, pix = e - q * PLANE, pr = pix / PC, pc = pix - pr * PC;
+        u32x2 a, b, c;
+        split3(v[i], a, b, c);
+        const int ent = buf * BUF + xw_pos(pr, pc);
+        l2[(ent + 0 * PLANE) * 2 + q] = a;
+        l2[(ent + 1 * PLANE) * 2 + q] = b;
+        l2[(ent + 2 * PLANE) * 2 + q] = c;
+      }
+    }
+  };
+  const int total = (nch >> 1) * 25 + (nch & 1) * NS;   // global K steps (chunk pairs, then a lone chunk)
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps2 * 16));
+  const int wbase = cb * total * IT * 64 + chh * ITW * 64;
+  auto ldw = [&](bf16x8 (&a)[3], int g, int it) {   // output tile it (of this wave's two) at step g
+    const int f = wbase + min(g, total - 1) * IT * 64 + it * 64;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] = ld_bf8(wr, lane * 16, (int)((q * ps2 + f) * 16));
+  };
+  auto ldb = [&](bf16x8 (&b)[PT][3], int buf, int s) {
+    const int tap = min(2 * s + h, KS * KS - 1);   // tap 25: any finite operand (its weights are zero)
+    const int ky = tap / KS, kx = tap - ky * KS;
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int o = buf * BUF + (S * (PT * rp + t) + ky) * PC + (kx & 1) * PCE + j + (kx >> 1);
+      b[t][0] = f4_as_bf8(lds[o]);
+      b[t][1] = f4_as_bf8(lds[o + PLANE]);
+      b[t][2] = f4_as_bf8(lds[o + 2 * PLANE]);
+    }
+  };
+  f32x16 acc[PT][ITW];
+#pragma unroll
+  for (int t = 0; t < PT; ++t)
+#pragma unroll
+    for (int it = 0; it < ITW; ++it) acc[t][it] = f32x16{0};
+  bf16x8 w[ITW][3], bq[2][PT][3];
+  f32x4 v[NF];
+  // one K step: the MFMAs of both pixel tiles per output tile, each tile's fragment set refilled for step g + 1
+  // right after its last use (a ring: one step of prefetch distance)
+  auto mm = [&](const bf16x8 (&b)[PT][3], int g) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < ITW; ++it) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) acc[t][it] = mfma_x6(w[it], b[t], acc[t][it]);
+      ldw(w[it], g + 1, it);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // the 12 tap-pair steps (taps 2 s, 2 s + 1) of the chunk in buffer buf, global steps g0 .. g0 + 11; the other
+  // buffer's next chunk (loaded into v beforehand) is split into LDS after step 3 (waves 0-3) or 8 (waves 4-7)
+  auto run12 = [&](int buf, int g0, bool put, int pbuf) __attribute__((always_inline)) {
+    ldb(bq[0], buf, 0);
+#pragma unroll
+    for (int s = 0; s < 12; ++s) {
+      if (s + 1 < 12) ldb(bq[(s + 1) & 1], buf, s + 1);
+      mm(bq[s & 1], g0 + s);
+      if (s == 3 && chh == 0 && put) fill_put(pbuf, v);   // the partners split at different steps
+      if (s == 8 && chh == 1 && put) fill_put(pbuf, v);
+    }
+  };
+  fill_load(0, v);
+#pragma unroll
+  for (int it = 0; it < ITW; ++it) ldw(w[it], 0, it);
+  fill_put(0, v);
+  __syncthreads();
+  // K order: chunk PAIRS (2 cp in buffer 0, 2 cp + 1 in buffer 1): 12 tap pairs of the first, the cross step (tap
+  // 24 of both chunks, lane half h = chunk), 12 tap pairs of the second -- 25 steps per 16 channels, as many as
+  // 16-channel chunks x 25 taps (no zero tap)
+  const int npair = nch >> 1;
+#pragma unroll 1
+  for (int cp = 0; cp < npair; ++cp) {
+    const int g0 = cp * 25;
+    fill_load(2 * cp + 1, v);
+    run12(0, g0, true, 1);
+    __syncthreads();                      // chunk 2 cp + 1 is in buffer 1
+    {
+      bf16x8 bx[PT][3];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {      // the cross step: buffer h, tap 24 = (4, 4)
+        const int o = h * BUF + (S * (PT * rp + t) + 4) * PC + j + 2;   // ky = kx = 4: even column half
+        bx[t][0] = f4_as_bf8(lds[o]);
+        bx[t][1] = f4_as_bf8(lds[o + PLANE]);
+        bx[t][2] = f4_as_bf8(lds[o + 2 * PLANE]);
+      }
+      mm(bx, g0 + 12);
+    }
+    __syncthreads();                      // every wave is done with buffer 0
+    const bool more = 2 * cp + 2 < nch;
+    if (more) fill_load(2 * cp + 2, v);
+    run12(1, g0 + 13, more, 0);
+    __syncthreads();                      // chunk 2 cp + 2 is in buffer 0
+  }
+  if (nch & 1) {                          // a lone last chunk (buffer 0): 13 tap pairs, tap 25 a zero weight
+    const int g0 = npair * 25;
+    ldb(bq[0], 0, 0);
+#pragma unroll
+    for (int s = 0; s < 13; ++s) {
+      if (s + 1 < 13) ldb(bq[(s + 1) & 1], 0, s + 1);
+      mm(bq[s & 1], g0 + s);
+    }
+    __syncthreads();
+  }
+  // epilogue: the patch is dead, the LDS is the exchange area [wave][t][it][g][lane]
+  int oy[PT];
+  bool ok[PT];
+  const int ox = ox0 + j;
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    oy[t] = oy0 + PT * rp + t;
+    ok[t] = oy[t] < p.Hout && ox < p.Wout;
+  }
+  if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+      conv_epilogue<ITW, EPI, 0, false, 2>(p, acc[t], n, oy[t], ox, ok[t], cb * IT * 32 + chh * ITW * 32);
+  } else {
+    static_assert(EPI == EPI_GDN || EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD || EPI == EPI_IGDN,
+                  "conv_down_x6w epilogues: bias, GDN / IGDN, GDN / IGDN backward");
+    auto xch = [&](int wv, int t, int it, int g) -> f32x4& { return lds[(((wv * PT + t) * ITW + it) * 4 + g) * 64 + lane]; };
+    const unsigned plane = (unsigned)p.Hout * p.Wout;
+    const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+    auto ldg = [&](bf16x8 (&a)[3], int ct, int k) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        a[q] = ld_bf8(grs, lane * 16, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+    };
+    unsigned vo[PT], vl[PT];
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      vo[t] = ok[t] ? h * plane + pix_at(oy[t], ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u;
+      vl[t] = ok[t] ? vo[t] : 0x0FFFFFF0u;   // past the descriptor's range: loads return 0 (never stored)
+    }
+    // the 8 values (registers 8s..8s+7) of global channel tile itg, k-step s, pixel tile t: this wave's own
+    // channel tile from registers, the partner's from the exchange area
+    auto kvals = [&](int t, int k, float (&v)[8]) {
+      const int itg = k >> 1, s = k & 1, hw = itg / ITW, il = itg - hw * ITW;
+      if (hw == chh) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = acc[t][il][8 * s + e];
+      } else {
+        const f32x4 a = xch(wave ^ 4, t, il, 2 * s), b = xch(wave ^ 4, t, il, 2 * s + 1);
+        v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+        v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+      }
+    };
+    if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
+      const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+      const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout), ers = chan_rsrc(p.beta, p.Cout);
+#pragma unroll
+      for (int it = 0; it < ITW; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 bv = ld_chan4(brs, (chh * ITW + it) * 32 + 8 * g + 4 * h);
+#pragma unroll
+          for (int t = 0; t < PT; ++t) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[t][it][4 * g + e] += bv[e];
+            xch(wave, t, it, g) = f32x4{acc[t][it][4 * g], acc[t][it][4 * g + 1], acc[t][it][4 * g + 2],
+                                        acc[t][it][4 * g + 3]};
+          }
+        }
+      __syncthreads();
+#pragma unroll
+      for (int il = 0; il < ITW; ++il) {   // this wave's output channel tiles
+        const int ct = chh * ITW + il;
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 nx[PT];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int t = 0; t < PT; ++t) nx[t][4 * g + e] = ev[e];
+        }
+        bf16x8 ga[2][3];
+        ldg(ga[0], ct, 0);
+#pragma unroll
+        for (int k = 0; k < 2 * IT; ++k) {
+          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], ct, k + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < PT; ++t) {
+            float v[8];
+            kvals(t, k, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = v[e] * v[e];
+            bf16x8 xq[3];
+            split3x8(v, xq);
+            nx[t] = mfma_x6(ga[k & 1], xq, nx[t]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+          if (!ok[t]) continue;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 yv, sv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float nv = nx[t][4 * g + e];
+              const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+              sv[e] = sc;
+              yv[e] = acc[t][il][4 * g + e] * sc;
+            }
+            const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
+            if (p.save_s) SS.st(vo[t], ss, sv);
+            Y.st(vo[t], ss, yv);
+          }
+        }
+      }
+    } else {
+      const Img4 Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
+      // pass 1: t of this wave's channels into the exchange area, g*s in place of g
+#pragma unroll
+      for (int t = 0; t < PT; ++t)
+#pragma unroll
+        for (int it = 0; it < ITW; ++it) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int itg = chh * ITW + it;
+          f32x4 yq[4], sq[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            yq[g] = IX.ld(vl[t], (unsigned)(itg * 8 + 2 * g) * plane);
+            sq[g] = IS.ld(vl[t], (unsigned)(itg * 8 + 2 * g) * plane);
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4 tv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float sg = sq[g][e], rs = __builtin_amdgcn_rcpf(sg), xs = yq[g][e] * rs;
+              const float gx = acc[t][it][4 * g + e] * xs;
+              tv[e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : (0.5f * gx) * rs;
+              float gs = acc[t][it][4 * g + e] * sg;
+              asm volatile("" : "+v"(gs));   // g*s rounded on its own: never contracted into dx's fma
+              acc[t][it][4 * g + e] = gs;
+            }
+            xch(wave, t, it, g) = tv;
+          }
+        }
+      __syncthreads();
+      // pass 2: u for this wave's output channel tiles over all 128 channels of t (exchange area), then
+      // dx = g*s + 2 y rcp(s) u
+#pragma unroll
+      for (int il = 0; il < ITW; ++il) {
+        const int jt = chh * ITW + il;
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 ux[PT];
+#pragma unroll
+        for (int t = 0; t < PT; ++t) ux[t] = f32x16{0};
+        bf16x8 ga[2][3];
+        ldg(ga[0], jt, 0);
+#pragma unroll
+        for (int k = 0; k < 2 * IT; ++k) {
+          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], jt, k + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          const int itg = k >> 1, s = k & 1, hw = itg / ITW, ilk = itg - hw * ITW;
+#pragma unroll
+          for (int t = 0; t < PT; ++t) {
+            const f32x4 a = xch(hw == chh ? wave : (wave ^ 4), t, ilk, 2 * s),
+                        b = xch(hw == chh ? wave : (wave ^ 4), t, ilk, 2 * s + 1);
+            const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+            bf16x8 tq[3];
+            split3x8(v, tq);
+            ux[t] = mfma_x6(ga[k & 1], tq, ux[t]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+          if (!ok[t]) continue;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const unsigned ss = (unsigned)(jt * 8 + 2 * g) * plane;
+            const f32x4 yv = IX.ld(vo[t], ss), sv = IS.ld(vo[t], ss);
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float x2 = 2.0f * (yv[e] * __builtin_amdgcn_rcpf(sv[e]));
+              asm volatile("" : "+v"(x2));   // as in the wide form: 2x materialised, then one fma with u
+              o[e] = acc[t][il][4 * g + e] + x2 * ux[t][4 * g + e];
+            }
+            Y.st(vo[t], ss, o);
+          }
+        }
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------------------------
 // conv_rgb_x6: the k5 s2 conv whose input is an RGB-sized map (Cin <= 4: g_a.0 forward, the g_s.6 input gradient)
 // as its PixelUnshuffle(2) view: a k3 s1 p1 conv over 16 virtual channels c' = 4 (2 sy + sx) + c at the output
 // resolution, x'[c'][u][v] = x[c][2u + sy][2v + sx]; the weight (ica_pack_conv_weight_x6 of w'[o][c'][ty][tx] =
@@ -966,6 +1333,44 @@ __global__ void pack_conv_x6_kernel(const float* __restrict__ w, __bf16* __restr
   dst[2 * total + i] = (__bf16)(r1 - (float)b);
 }
 
+// tap-pair fragments of conv_down_x6w, [cb][chunk8][step][it][lane][e] (three split planes): lane (h, r) supplies
+// A[r][k = 8 h + e] = W[o][c = 8 chunk8 + e][tap = 2 step + h], 0 past C and for tap 25
+__global__ void pack_conv_x6w_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int O, int C, long so,
+                                     long sc, int IT, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int nch8 = ((C + 3) / 4 + 1) / 2, npair = nch8 >> 1;
+  const int nsteps = npair * 25 + (nch8 & 1) * XW_NS;
+  long t = i;
+  const int e = t % 8; t /= 8;
+  const int lane = t % 64; t /= 64;
+  const int it = t % IT; t /= IT;
+  const int g = t % nsteps;
+  const int cb = (int)(t / nsteps);
+  const int h = lane >> 5;
+  // step g -> (8-channel chunk, tap) of lane half h: chunk pairs of 25 steps (12 tap pairs of chunk 2 cp, the cross
+  // step = tap 24 of chunk 2 cp + h, 12 tap pairs of chunk 2 cp + 1), then a lone chunk's 13 tap pairs
+  int c8, tap;
+  if (g < npair * 25) {
+    const int cp = g / 25, sl = g - cp * 25;
+    if (sl < 12) { c8 = 2 * cp; tap = 2 * sl + h; }
+    else if (sl == 12) { c8 = 2 * cp + h; tap = 24; }
+    else { c8 = 2 * cp + 1; tap = 2 * (sl - 13) + h; }
+  } else {
+    c8 = nch8 - 1;
+    tap = 2 * (g - npair * 25) + h;
+  }
+  const int o = cb * IT * 32 + it * 32 + (lane & 31), c = c8 * 8 + e;
+  float v = 0.f;
+  if (o < O && c < C && tap < 25) v = w[o * so + c * sc + tap];
+  const __bf16 a = (__bf16)v;
+  const float r1 = v - (float)a;
+  const __bf16 b = (__bf16)r1;
+  dst[i] = a;
+  dst[total + i] = b;
+  dst[2 * total + i] = (__bf16)(r1 - (float)b);
+}
+
 // the fp32 gamma' pack of ica_pack_gdn ([a][b][lane][r]) -> three bf16 planes [plane][a][b][s][lane][e], r = 8s + e
 // (the epilogue's k-step s of tile b, lane order unchanged)
 __global__ void pack_gdn_x6_kernel(const float* __restrict__ gp, __bf16* __restrict__ dst, long total) {
@@ -992,6 +1397,27 @@ int launch_down_x6_pt(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
+// fragments of the order-0 x6 pack per plane, and of the tap-pair extension conv_down_x6w reads (KS = 5, IT = 4)
+static inline long x6_plane_frags(int O, int C, int KS, int IT) {
+  return (long)((O + IT * 32 - 1) / (IT * 32)) * ((((C + 3) / 4) * 4 + 15) / 16) * KS * KS * IT * 64;
+}
+static inline long x6w_plane_frags(int O, int C) {
+  const int nch8 = ((C + 3) / 4 + 1) / 2;
+  return (long)((O + 127) / 128) * ((nch8 >> 1) * 25 + (nch8 & 1) * XW_NS) * 4 * 64;
+}
+
+template <int EPI, int PT>
+int launch_down_x6w(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + 4 * PT - 1) / (4 * PT)) * p.N;
+  const int ncb = (p.Cout + 127) / 128;
+  ConvParams q = p;
+  q.wp = reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.wp) +
+                                        3 * x6_plane_frags(p.Cout, p.Cin, 5, 4) * 16);
+  ICA_LAUNCH((conv_down_x6w_kernel<EPI, PT>), dim3(tiles, ncb), dim3(512), 0, st, q, x6w_plane_frags(p.Cout, p.Cin));
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
 constexpr int XS_SMALL_PX = 32 * 32;   // the small-grid x6 kernels: low-resolution side <= 32 x 32 per image
 
 template <int IT, int EPI>
@@ -1013,6 +1439,10 @@ int launch_down_x6(const ConvParams& p, hipStream_t st) {
   if (p.Hout * p.Wout <= XS_SMALL_PX) return launch_down_small_x6<IT, EPI>(p, st);
   const int blocks2 = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + xd_th<X6_PT>() - 1) / xd_th<X6_PT>()) * p.N *
                       ((p.Cout + IT * 32 - 1) / (IT * 32));
+  if constexpr (IT == 4) {   // 128 output channels: the 8-wave kernel
+    if (blocks2 < 256) return launch_down_x6w<EPI, 1>(p, st);
+    return launch_down_x6w<EPI, 2>(p, st);
+  }
   if (blocks2 < 256) return launch_down_x6_pt<IT, EPI, 1>(p, st);
   return launch_down_x6_pt<IT, EPI, X6_PT>(p, st);
 }
@@ -1170,9 +1600,8 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
 extern "C" {
 
 size_t ica_pack_conv_weight_x6_size(int O, int C, int KS, int IT) {
-  const int ncb = (O + IT * 32 - 1) / (IT * 32);
-  const int nch = (((C + 3) / 4) * 4 + 15) / 16;
-  return (size_t)3 * ncb * nch * KS * KS * IT * 64 * 8;
+  // the 16-channel-chunk pack, plus (KS = 5, IT = 4) the tap-pair pack of conv_down_x6w behind it
+  return (size_t)3 * 8 * (x6_plane_frags(O, C, KS, IT) + (KS == 5 && IT == 4 ? x6w_plane_frags(O, C) : 0));
 }
 
 size_t ica_pack_gdn_x6_size(int C) { return (size_t)3 * (C / 32) * (C / 32) * 2048; }
@@ -1192,10 +1621,16 @@ int ica_pack_gdn_x6(const float* gp, void* dst, int C, hipStream_t st) {
 int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
                             hipStream_t st) {
   if (it <= 0) return -3;
-  const long total = (long)ica_pack_conv_weight_x6_size(O, C, KS, it) / 3;
+  const long total = x6_plane_frags(O, C, KS, it) * 8;
   ICA_LAUNCH(pack_conv_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, it, order, total);
   ICA_CHECK_LAUNCH();
+  if (KS == 5 && it == 4 && order == 0) {   // conv_down_x6w's tap-pair pack (conv_up packs leave it unused)
+    const long t2 = x6w_plane_frags(O, C) * 8;
+    ICA_LAUNCH(pack_conv_x6w_kernel, dim3((t2 + 255) / 256), dim3(256), 0, st, w,
+               reinterpret_cast<__bf16*>(dst) + 3 * total, O, C, so, sc, it, t2);
+    ICA_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -70,7 +70,9 @@ int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* b
 /* fp32-accurate bf16x6 packs for ica_conv_ex launches with prec = 2 (ica_conv_x6.hip; the anchors/utils.py:112-130
  * k5 s2 conv / deconv layers of g_a and g_s and their input gradients).  Each weight w is split exactly into three
  * bf16 parts w = hi + mid + lo; dst holds three planes (hi, mid, lo), each in the CC = 16 fragment order of
- * ica_pack_conv_weight (order 0: conv_down, 1: conv_up) with row tiles it (> 0);
+ * ica_pack_conv_weight (order 0: conv_down, 1: conv_up) with row tiles it (> 0).  For KS = 5, it = 4 the buffer
+ * continues with the tap-pair pack of the 8-wave conv_down (three planes of [cb][K step][it][lane] fragments; lane half
+ * h of a step = tap 2 s + h of an 8-channel chunk, chunk pairs sharing a tap-24 step; filled for order 0);
  * ica_pack_conv_weight_x6_size(O, C, KS, it) bf16 values in all. */
 int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
                             hipStream_t stream);
