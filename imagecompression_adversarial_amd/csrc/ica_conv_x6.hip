@@ -197,6 +197,201 @@ __device__ __forceinline__ int xw_pos(int pr, int pc) {   // LDS entry of patch 
   constexpr int PC = 2 * 31 + 5, PCE = (PC + 1) / 2;
   return pr * PC + ((pc & 1) ? PCE + (pc >> 1) : (pc >> 1));
 }
+// Epilogue of the 8-wave x6 conv_down (conv_down_x6w): this wave's PT pixel tiles x 64 output channels
+// (half chh; the SIMD partner wave ^ 4 holds the other half of the same pixels).  The block's LDS, free by now,
+// is the exchange area [wave][t][it][g][lane]: each wave publishes what the partner's channels need (GDN / IGDN:
+// x = conv + bias; the GDN / IGDN backward: t) and reads the partner's, so the normaliser GEMMs over all 128
+// channels run with the arithmetic and MFMA order of the single-wave epilogues (gdn_fwd_x6_pair / the wide
+// backward).  All waves of the block call it (it holds a block barrier).  (The same epilogue behind a conv_up whose
+// SIMD partners split the output channels, both classes accumulated first, measured 2-4 % slower than
+// conv_up_x6w / conv_up_x6 on every layer: conv_up has no patch refill for a double buffer to hide.)
+template <int EPI, int PT>
+ICA_DEV void xw_epilogue(const ConvParams& p, f32x16 (&acc)[PT][2], int n, const int (&oy)[PT], int ox,
+                         const bool (&ok)[PT], int chh, int wave, int cb, f32x4* lds) {
+  constexpr int IT = 4, ITW = 2;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+  for (int t = 0; t < PT; ++t)
+    conv_epilogue<ITW, EPI, 0, false, 2>(p, acc[t], n, oy[t], ox, ok[t], cb * IT * 32 + chh * ITW * 32);
+} else {
+  static_assert(EPI == EPI_GDN || EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD || EPI == EPI_IGDN,
+                "conv_down_x6w epilogues: bias, GDN / IGDN, GDN / IGDN backward");
+  auto xch = [&](int wv, int t, int it, int g) -> f32x4& { return lds[(((wv * PT + t) * ITW + it) * 4 + g) * 64 + lane]; };
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+  auto ldg = [&](bf16x8 (&a)[3], int ct, int k) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      a[q] = ld_bf8(grs, lane * 16, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+  };
+  unsigned vo[PT], vl[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    vo[t] = ok[t] ? h * plane + pix_at(oy[t], ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u;
+    vl[t] = ok[t] ? vo[t] : 0x0FFFFFF0u;   // past the descriptor's range: loads return 0 (never stored)
+  }
+  // the 8 values (registers 8s..8s+7) of global channel tile itg, k-step s, pixel tile t: this wave's own
+  // channel tile from registers, the partner's from the exchange area
+  auto kvals = [&](int t, int k, float (&v)[8]) {
+    const int itg = k >> 1, s = k & 1, hw = itg / ITW, il = itg - hw * ITW;
+    if (hw == chh) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = acc[t][il][8 * s + e];
+    } else {
+      const f32x4 a = xch(wave ^ 4, t, il, 2 * s), b = xch(wave ^ 4, t, il, 2 * s + 1);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+      v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+    }
+  };
+  if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
+    const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+    const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout), ers = chan_rsrc(p.beta, p.Cout);
+#pragma unroll
+    for (int it = 0; it < ITW; ++it)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bv = ld_chan4(brs, (chh * ITW + it) * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[t][it][4 * g + e] += bv[e];
+          xch(wave, t, it, g) = f32x4{acc[t][it][4 * g], acc[t][it][4 * g + 1], acc[t][it][4 * g + 2],
+                                      acc[t][it][4 * g + 3]};
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int il = 0; il < ITW; ++il) {   // this wave's output channel tiles
+      const int ct = chh * ITW + il;
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 nx[PT];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int t = 0; t < PT; ++t) nx[t][4 * g + e] = ev[e];
+      }
+      bf16x8 ga[2][3];
+      ldg(ga[0], ct, 0);
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], ct, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+          float v[8];
+          kvals(t, k, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] * v[e];
+          bf16x8 xq[3];
+          split3x8(v, xq);
+          nx[t] = mfma_x6(ga[k & 1], xq, nx[t]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        if (!ok[t]) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 yv, sv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float nv = nx[t][4 * g + e];
+            const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+            sv[e] = sc;
+            yv[e] = acc[t][il][4 * g + e] * sc;
+          }
+          const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
+          if (p.save_s) SS.st(vo[t], ss, sv);
+          Y.st(vo[t], ss, yv);
+        }
+      }
+    }
+  } else {
+    const Img4 Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
+    // pass 1: t of this wave's channels into the exchange area, g*s in place of g
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int it = 0; it < ITW; ++it) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int itg = chh * ITW + it;
+        f32x4 yq[4], sq[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          yq[g] = IX.ld(vl[t], (unsigned)(itg * 8 + 2 * g) * plane);
+          sq[g] = IS.ld(vl[t], (unsigned)(itg * 8 + 2 * g) * plane);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 tv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sg = sq[g][e], rs = __builtin_amdgcn_rcpf(sg), xs = yq[g][e] * rs;
+            const float gx = acc[t][it][4 * g + e] * xs;
+            tv[e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : (0.5f * gx) * rs;
+            float gs = acc[t][it][4 * g + e] * sg;
+            asm volatile("" : "+v"(gs));   // g*s rounded on its own: never contracted into dx's fma
+            acc[t][it][4 * g + e] = gs;
+          }
+          xch(wave, t, it, g) = tv;
+        }
+      }
+    __syncthreads();
+    // pass 2: u for this wave's output channel tiles over all 128 channels of t (exchange area), then
+    // dx = g*s + 2 y rcp(s) u
+#pragma unroll
+    for (int il = 0; il < ITW; ++il) {
+      const int jt = chh * ITW + il;
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 ux[PT];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) ux[t] = f32x16{0};
+      bf16x8 ga[2][3];
+      ldg(ga[0], jt, 0);
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], jt, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const int itg = k >> 1, s = k & 1, hw = itg / ITW, ilk = itg - hw * ITW;
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+          const f32x4 a = xch(hw == chh ? wave : (wave ^ 4), t, ilk, 2 * s),
+                      b = xch(hw == chh ? wave : (wave ^ 4), t, ilk, 2 * s + 1);
+          const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+          bf16x8 tq[3];
+          split3x8(v, tq);
+          ux[t] = mfma_x6(ga[k & 1], tq, ux[t]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        if (!ok[t]) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const unsigned ss = (unsigned)(jt * 8 + 2 * g) * plane;
+          const f32x4 yv = IX.ld(vo[t], ss), sv = IS.ld(vo[t], ss);
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x2 = 2.0f * (yv[e] * __builtin_amdgcn_rcpf(sv[e]));
+            asm volatile("" : "+v"(x2));   // as in the wide form: 2x materialised, then one fma with u
+            o[e] = acc[t][il][4 * g + e] + x2 * ux[t][4 * g + e];
+          }
+          Y.st(vo[t], ss, o);
+        }
+      }
+    }
+  }
+}
+}
+
 // PT = 2: 8 x 32 output pixels per block, two rows per wave; PT = 1 (4 x 32, one row per wave) where the PT = 2 grid
 // leaves CUs idle.  Both run the same MFMA and epilogue sequence per output (same bits at any batch size).
 
@@ -354,186 +549,7 @@ __global__ __launch_bounds__(512, 1) void conv_down_x6w_kernel(ConvParams p, lon
     oy[t] = oy0 + PT * rp + t;
     ok[t] = oy[t] < p.Hout && ox < p.Wout;
   }
-  if constexpr (EPI == EPI_BIAS) {
-#pragma unroll
-    for (int t = 0; t < PT; ++t)
-      conv_epilogue<ITW, EPI, 0, false, 2>(p, acc[t], n, oy[t], ox, ok[t], cb * IT * 32 + chh * ITW * 32);
-  } else {
-    static_assert(EPI == EPI_GDN || EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD || EPI == EPI_IGDN,
-                  "conv_down_x6w epilogues: bias, GDN / IGDN, GDN / IGDN backward");
-    auto xch = [&](int wv, int t, int it, int g) -> f32x4& { return lds[(((wv * PT + t) * ITW + it) * 4 + g) * 64 + lane]; };
-    const unsigned plane = (unsigned)p.Hout * p.Wout;
-    const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
-    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
-    auto ldg = [&](bf16x8 (&a)[3], int ct, int k) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        a[q] = ld_bf8(grs, lane * 16, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
-    };
-    unsigned vo[PT], vl[PT];
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      vo[t] = ok[t] ? h * plane + pix_at(oy[t], ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u;
-      vl[t] = ok[t] ? vo[t] : 0x0FFFFFF0u;   // past the descriptor's range: loads return 0 (never stored)
-    }
-    // the 8 values (registers 8s..8s+7) of global channel tile itg, k-step s, pixel tile t: this wave's own
-    // channel tile from registers, the partner's from the exchange area
-    auto kvals = [&](int t, int k, float (&v)[8]) {
-      const int itg = k >> 1, s = k & 1, hw = itg / ITW, il = itg - hw * ITW;
-      if (hw == chh) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = acc[t][il][8 * s + e];
-      } else {
-        const f32x4 a = xch(wave ^ 4, t, il, 2 * s), b = xch(wave ^ 4, t, il, 2 * s + 1);
-        v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
-        v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
-      }
-    };
-    if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
-      const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
-      const __amdgpu_buffer_rsrc_t brs = chan_rsrc(p.bias, p.Cout), ers = chan_rsrc(p.beta, p.Cout);
-#pragma unroll
-      for (int it = 0; it < ITW; ++it)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 bv = ld_chan4(brs, (chh * ITW + it) * 32 + 8 * g + 4 * h);
-#pragma unroll
-          for (int t = 0; t < PT; ++t) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[t][it][4 * g + e] += bv[e];
-            xch(wave, t, it, g) = f32x4{acc[t][it][4 * g], acc[t][it][4 * g + 1], acc[t][it][4 * g + 2],
-                                        acc[t][it][4 * g + 3]};
-          }
-        }
-      __syncthreads();
-#pragma unroll
-      for (int il = 0; il < ITW; ++il) {   // this wave's output channel tiles
-        const int ct = chh * ITW + il;
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 nx[PT];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 ev = ld_chan4(ers, ct * 32 + 8 * g + 4 * h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int t = 0; t < PT; ++t) nx[t][4 * g + e] = ev[e];
-        }
-        bf16x8 ga[2][3];
-        ldg(ga[0], ct, 0);
-#pragma unroll
-        for (int k = 0; k < 2 * IT; ++k) {
-          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], ct, k + 1);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int t = 0; t < PT; ++t) {
-            float v[8];
-            kvals(t, k, v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = v[e] * v[e];
-            bf16x8 xq[3];
-            split3x8(v, xq);
-            nx[t] = mfma_x6(ga[k & 1], xq, nx[t]);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < PT; ++t) {
-          if (!ok[t]) continue;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 yv, sv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float nv = nx[t][4 * g + e];
-              const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
-              sv[e] = sc;
-              yv[e] = acc[t][il][4 * g + e] * sc;
-            }
-            const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
-            if (p.save_s) SS.st(vo[t], ss, sv);
-            Y.st(vo[t], ss, yv);
-          }
-        }
-      }
-    } else {
-      const Img4 Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
-      // pass 1: t of this wave's channels into the exchange area, g*s in place of g
-#pragma unroll
-      for (int t = 0; t < PT; ++t)
-#pragma unroll
-        for (int it = 0; it < ITW; ++it) {
-          __builtin_amdgcn_sched_barrier(0);
-          const int itg = chh * ITW + it;
-          f32x4 yq[4], sq[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            yq[g] = IX.ld(vl[t], (unsigned)(itg * 8 + 2 * g) * plane);
-            sq[g] = IS.ld(vl[t], (unsigned)(itg * 8 + 2 * g) * plane);
-          }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            f32x4 tv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float sg = sq[g][e], rs = __builtin_amdgcn_rcpf(sg), xs = yq[g][e] * rs;
-              const float gx = acc[t][it][4 * g + e] * xs;
-              tv[e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : (0.5f * gx) * rs;
-              float gs = acc[t][it][4 * g + e] * sg;
-              asm volatile("" : "+v"(gs));   // g*s rounded on its own: never contracted into dx's fma
-              acc[t][it][4 * g + e] = gs;
-            }
-            xch(wave, t, it, g) = tv;
-          }
-        }
-      __syncthreads();
-      // pass 2: u for this wave's output channel tiles over all 128 channels of t (exchange area), then
-      // dx = g*s + 2 y rcp(s) u
-#pragma unroll
-      for (int il = 0; il < ITW; ++il) {
-        const int jt = chh * ITW + il;
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 ux[PT];
-#pragma unroll
-        for (int t = 0; t < PT; ++t) ux[t] = f32x16{0};
-        bf16x8 ga[2][3];
-        ldg(ga[0], jt, 0);
-#pragma unroll
-        for (int k = 0; k < 2 * IT; ++k) {
-          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], jt, k + 1);
-          __builtin_amdgcn_sched_barrier(0);
-          const int itg = k >> 1, s = k & 1, hw = itg / ITW, ilk = itg - hw * ITW;
-#pragma unroll
-          for (int t = 0; t < PT; ++t) {
-            const f32x4 a = xch(hw == chh ? wave : (wave ^ 4), t, ilk, 2 * s),
-                        b = xch(hw == chh ? wave : (wave ^ 4), t, ilk, 2 * s + 1);
-            const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-            bf16x8 tq[3];
-            split3x8(v, tq);
-            ux[t] = mfma_x6(ga[k & 1], tq, ux[t]);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < PT; ++t) {
-          if (!ok[t]) continue;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const unsigned ss = (unsigned)(jt * 8 + 2 * g) * plane;
-            const f32x4 yv = IX.ld(vo[t], ss), sv = IS.ld(vo[t], ss);
-            f32x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float x2 = 2.0f * (yv[e] * __builtin_amdgcn_rcpf(sv[e]));
-              asm volatile("" : "+v"(x2));   // as in the wide form: 2x materialised, then one fma with u
-              o[e] = acc[t][il][4 * g + e] + x2 * ux[t][4 * g + e];
-            }
-            Y.st(vo[t], ss, o);
-          }
-        }
-      }
-    }
-  }
+  xw_epilogue<EPI, PT>(p, acc, n, oy, ox, ok, chh, wave, cb, lds);
 }
 
 // --------------------------------------------------------------------------------------------------------------
