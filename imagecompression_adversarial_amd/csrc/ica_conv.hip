@@ -87,7 +87,11 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
   // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
   static_assert(!X6O || (!BF && CC == 16), "x6 conv_down: fp32 fills of 16-channel chunks");
-  __shared__ f32x4 patch[X6O ? 6 * PLANE : NE * PLANE];   // X6O: [plane][half][pixel], 8 channels as bf16
+#ifndef ICA_X6O_SB
+  __shared__ f32x4 patch[X6O ? 12 * PLANE : NE * PLANE];   // X6O: [buffer][plane][half][pixel], 8 channels as bf16
+#else
+  __shared__ f32x4 patch[X6O ? 6 * PLANE : NE * PLANE];
+#endif
   // bf16 16-channel-chunk layers: the epilogue parameters in LDS (epi_params_to_lds), copied before the first
   // chunk fill, whose barriers publish them
   // The RGB-input GDN forward too (g_a.0: 1.65 -> 1.31 ms at the config-5 shapes, although its 46 KB of LDS take it
@@ -454,6 +458,93 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
 #pragma unroll
         for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
     };
+    // Double-buffered patch (X6DB): chunk c + 1 is staged into the other 6-plane buffer while chunk c's taps run
+    // -- its NF quads per thread are issued one per tap (taps 0..NF-1, after that tap's weight prefetch) and split
+    // into the bf16 planes PUTD taps later -- so one barrier per chunk and no exposed fill latency.  The weights
+    // run in a 3-set ring two taps ahead (KK = 9 = 3 rings, so a chunk always starts on set 0): a tap's fill load
+    // is then younger than the weights consumed for the next three taps, and the in-order vmcnt never waits on it
+    // before its own split.  Same MFMA order as the single-buffer loop (bit-identical results).
+#ifndef ICA_X6O_SB
+    static_assert(KK % 3 == 0, "x6 conv_down ring: KK a multiple of 3");
+    constexpr bool MK = (FX & FX_MASK) != 0, US = (FX & FX_UNSHUF) != 0;
+    constexpr int NF = (NE * PLANE + 255) / 256, PUTD = 3;
+    static_assert(NF + PUTD <= KK, "x6 conv_down: the chunk's fill must land inside its taps");
+    const unsigned xplane = (unsigned)p.Hin * p.Win;
+    const __amdgpu_buffer_rsrc_t xr =
+        uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
+    const __amdgpu_buffer_rsrc_t mr =
+        uniform_rsrc(reinterpret_cast<const char*>(MK ? p.mask : p.x) + (size_t)n * Cin4 * xplane * 16,
+                     MK ? Cin4 * xplane * 16u : 0u);
+    // per-thread quad offsets (chunk 0) and validity: a quad's offset is linear in the chunk (4 quads a chunk) in
+    // both views (plain: 4 channel planes; PixelUnshuffle(2): one quad plane of the 2x tensor = 4 Hin Win quads)
+    unsigned fo[NF];
+    int fq[NF];
+    bool fok[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
+      const int iy = iy0 + pr, ix = ix0 + pc;
+      fq[i] = q;
+      fok[i] = e < NE * PLANE && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      if constexpr (US)
+        fo[i] = (((unsigned)(2 * iy + (q >> 1))) * (2 * p.Win) + 2 * ix + (q & 1)) * 16u;
+      else
+        fo[i] = ((unsigned)q * xplane + pix_at(iy, ix, p.Hin, p.Win, p.pl & PL_IN)) * 16u;
+    }
+    u32x4_t fv[NF], fm[MK ? NF : 1];
+    auto fload = [&](int ch, int i) {
+      const bool ok = fok[i] && ch * NQ + fq[i] < Cin4;
+      const unsigned vo = ok ? fo[i] + (unsigned)ch * 4u * xplane * 16u : 0xFFFFFFF0u;
+      fv[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, 0, 0));
+      if constexpr (MK) fm[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(mr, vo, 0, 0));
+    };
+    auto fput = [&](f32x4* buf, int i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e < NE * PLANE) {   // quad q of pixel pix -> three bf16 planes, half q >> 1, slot q & 1
+        const int q = fq[i], pix = e - q * PLANE;
+        f32x4 x = __builtin_bit_cast(f32x4, fv[i]);
+        if constexpr (MK) {   // the generic fill's leaky-ReLU view, same fp32 ops
+          const f32x4 m = __builtin_bit_cast(f32x4, fm[i]);
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) x[e2] = m[e2] > 0.f ? x[e2] : x[e2] * 0.01f;
+        }
+        u32x2 a, b, c;
+        split3(x, a, b, c);
+        u32x2* p2 = reinterpret_cast<u32x2*>(buf);
+        const int ent = (q >> 1) * PLANE + pix;
+        p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
+        p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+        p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < NF; ++i) fload(0, i);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) fput(patch, i);
+    __syncthreads();
+    bf16x8 fr[3][IT][3];
+    ldw(fr[0], 0);
+    ldw(fr[1], 1);
+#pragma unroll 1
+    for (int ch = 0; ch < nch; ++ch) {
+      const f32x4* cur = patch + (ch & 1) * 6 * PLANE;
+      f32x4* nxt = patch + ((ch & 1) ^ 1) * 6 * PLANE;
+#pragma unroll
+      for (int tap = 0; tap < KK; ++tap) {
+        ldw(fr[(tap + 2) % 3], ch * KK + tap + 2);
+        if (tap < NF) fload(ch + 1, tap);   // past the last chunk: c4 >= Cin4, zero reads into the idle buffer
+        if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
+        __builtin_amdgcn_sched_barrier(0);
+        const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+        const int o = h * PLANE + lbase + ky * PC + kx;
+        const bf16x8 b[3] = {f4_as_bf8(cur[o]), f4_as_bf8(cur[2 * PLANE + o]), f4_as_bf8(cur[4 * PLANE + o])};
+#pragma unroll
+        for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(fr[tap % 3][it], b, acc[0][it]);
+      }
+      __syncthreads();
+    }
+#else
     auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) {
       const int ch = g / KK, tap = g - ch * KK;
       if (tap == 0) fill(ch);
@@ -474,6 +565,7 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
       step(fb, fa, g + 1);
     }
     if (g < total) step(fa, fb, g);
+#endif
   } else {
     // Weight fragments stream linearly through (chunk, tap); they are prefetched
     // one tap ahead into the other of two register sets (ping-pong, no copies)
