@@ -530,17 +530,25 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
     for (int ch = 0; ch < nch; ++ch) {
       const f32x4* cur = patch + (ch & 1) * 6 * PLANE;
       f32x4* nxt = patch + ((ch & 1) ^ 1) * 6 * PLANE;
+      // B operands: tap t + 1's three planes are read during tap t (tap 0's right after the barrier)
+      bf16x8 bb[2][3];
+      auto ldb = [&](bf16x8 (&b)[3], int tap) {
+        const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+        const int o = h * PLANE + lbase + ky * PC + kx;
+        b[0] = f4_as_bf8(cur[o]);
+        b[1] = f4_as_bf8(cur[2 * PLANE + o]);
+        b[2] = f4_as_bf8(cur[4 * PLANE + o]);
+      };
+      ldb(bb[0], 0);
 #pragma unroll
       for (int tap = 0; tap < KK; ++tap) {
         ldw(fr[(tap + 2) % 3], ch * KK + tap + 2);
         if (tap < NF) fload(ch + 1, tap);   // past the last chunk: c4 >= Cin4, zero reads into the idle buffer
         if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
+        if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
         __builtin_amdgcn_sched_barrier(0);
-        const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-        const int o = h * PLANE + lbase + ky * PC + kx;
-        const bf16x8 b[3] = {f4_as_bf8(cur[o]), f4_as_bf8(cur[2 * PLANE + o]), f4_as_bf8(cur[4 * PLANE + o])};
 #pragma unroll
-        for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(fr[tap % 3][it], b, acc[0][it]);
+        for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(fr[tap % 3][it], bb[tap & 1], acc[0][it]);
       }
       __syncthreads();
     }
