@@ -618,7 +618,10 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = oy0 + oyl[t], ox = ox0 + oxl[t];
-    conv_epilogue<IT, EPI, FX, BF, 0, LG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lpar);
+    // X6O: the GDN / IGDN (and backward) normaliser GEMMs on x6 operands too (wide form, 1 wave/SIMD; the gamma' pack
+    // of ica_pack_gdn_x6)
+    constexpr int EX6 = X6O && epi_gdn<EPI>() ? 1 : 0;
+    conv_epilogue<IT, EPI, FX, BF, EX6, LG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lpar);
   }
 }
 

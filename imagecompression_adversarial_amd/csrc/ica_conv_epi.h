@@ -630,7 +630,9 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         }
       }
     } else {
-      static_assert(!X6, "x6 GDN-bwd epilogue: plain layers, IT <= 4");
+      // x6 (the cheng2020 k3 s1 kernels: residual gradient, C = 192): the same two-pass flow, u = gamma'^T t on x6
+      // operands in the wide form (t split into three planes as it is formed, every output tile at once)
+      static_assert(X6 != 2 && (X6 == 0 || (!BF && (FX & FX_T) == 0)), "x6 GDN-bwd epilogue: wide form, no t output");
       if constexpr ((FX & FX_RES) != 0) {
         const Img SX(p.save_x, img, n), RS(p.res, img, n);
   #pragma unroll
@@ -666,8 +668,10 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       // the parity tests were pinned with.  bf16 path: GDN -0.5 g y s^2, IGDN 0.5 g y rcp(s)^2 (v_rcp_f32; the
       // epilogue was VALU-bound on division sequences), and t goes straight into its hi/lo B fragments
       // (register r = 4g+e is k-step r>>3, element r&7), no fp32 copy kept.
-      f32x16 tt[BF ? 1 : IT];
+      f32x16 tt[(BF || X6) ? 1 : IT];
       bf16x8 th[BF ? IT : 1][2], tl[BF ? IT : 1][2];
+      bf16x8 tq[X6 == 1 ? IT : 1][2][3];   // x6: t of k-step s (registers 8s..8s+7) as three bf16 planes
+      float tw[8];
       const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
   #pragma unroll
       for (int it = 0; it < IT; ++it)
@@ -699,20 +703,48 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
               split_bf(t, hi, lo);
               th[it][g >> 1][4 * (g & 1) + e] = hi;
               tl[it][g >> 1][4 * (g & 1) + e] = lo;
+            } else if constexpr (X6 == 1) {
+              tw[4 * (g & 1) + e] = t;
             } else {
               tt[it][4 * g + e] = t;
             }
+          }
+          if constexpr (X6 == 1) {
+            if (g & 1) split3x8(tw, tq[it][g >> 1]);
           }
           if constexpr ((FX & FX_T) != 0) {
             if (valid) ST.st(vo, ss, tv);
           }
         }
-      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
+      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, X6 ? IT * IT * 6144 : IT * IT * 4096);
+      f32x16 ux[X6 == 1 ? IT : 1];
+      if constexpr (X6 == 1) {   // round k = (k-tile ct, k-step s) feeds every output tile; fragments a round ahead
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jt = 0; jt < IT; ++jt) ux[jt] = f32x16{0};
+        bf16x8 ga[2][IT][3];
+        auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
+#pragma unroll
+          for (int jt = 0; jt < IT; ++jt)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              a[jt][q] = ld_bf8(grs, lane * 16, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+        };
+        ldg(ga[0], 0);
+#pragma unroll
+        for (int k = 0; k < 2 * IT; ++k) {
+          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int jt = 0; jt < IT; ++jt) ux[jt] = mfma_x6(ga[k & 1][jt], tq[k >> 1][k & 1], ux[jt]);
+        }
+      }
   #pragma unroll
       for (int jt = 0; jt < IT; ++jt) {
         f32x16 uacc = f32x16{0};
+        if constexpr (X6 == 1) uacc = ux[jt];
   #pragma unroll
-        for (int ct = 0; ct < IT; ++ct) {
+        for (int ct = 0; ct < (X6 ? 0 : IT); ++ct) {
           if constexpr (BF) {
             const int o = (jt * IT + ct) * 4096;
   #pragma unroll

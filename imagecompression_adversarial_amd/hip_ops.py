@@ -505,10 +505,10 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
         if prec == PREC_BF16:
             gdn.bf16()
             gp = gdn.gpbT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpb
-        elif prec == PREC_X6 and KS == 5:
+        elif prec == PREC_X6:   # x6 epilogue GEMMs (k5 s2 and, since round 4, the k3 s1 conv_downs)
             gdn.x6()
             gp = gdn.gpxT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpx
-        else:   # fp32 epilogues (fp32 operands, and the x6 k3 s1 conv_downs: fp32 gamma' GEMMs)
+        else:   # fp32 epilogues (fp32 operands)
             gp = gdn.gpT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gp
     a = ConvArgs(ptr(x4), ptr(y), ptr(wp), ptr(bias), ptr(gp), ptr(None if gdn is None else gdn.beta), ptr(save_x),
                  ptr(save_s), ptr(in_x), ptr(in_s), ptr(save_t), ptr(res), ptr(mask), N, Cin, H, W, Cout, Ho, Wo,
