@@ -88,7 +88,10 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
   static_assert(!X6O || (!BF && CC == 16), "x6 conv_down: fp32 fills of 16-channel chunks");
 #ifndef ICA_X6O_SB
-  __shared__ f32x4 patch[X6O ? 12 * PLANE : NE * PLANE];   // X6O: [buffer][plane][half][pixel], 8 channels as bf16
+  // X6O: [buffer][plane][half][pixel], 8 channels as bf16; the GDN-backward epilogues park g*s in it afterwards
+  // (IT*16 floats per lane, one slab per wave)
+  constexpr bool XST = X6O && (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) && !(FX == 0 && IT <= 4);
+  __shared__ f32x4 patch[X6O ? (XST && IT * 1024 > 12 * PLANE ? IT * 1024 : 12 * PLANE) : NE * PLANE];
 #else
   __shared__ f32x4 patch[X6O ? 6 * PLANE : NE * PLANE];
 #endif
@@ -621,7 +624,8 @@ __global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF
     // X6O: the GDN / IGDN (and backward) normaliser GEMMs on x6 operands too (wide form, 1 wave/SIMD; the gamma' pack
     // of ica_pack_gdn_x6)
     constexpr int EX6 = X6O && epi_gdn<EPI>() ? 1 : 0;
-    conv_epilogue<IT, EPI, FX, BF, EX6, LG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lpar);
+    conv_epilogue<IT, EPI, FX, BF, EX6, LG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lpar,
+                                            X6O ? reinterpret_cast<float*>(patch) + wave * IT * 1024 : nullptr);
   }
 }
 

@@ -167,7 +167,7 @@ ICA_DEV unsigned pix_at(int y, int x, int H, int W, bool split) {
 // global memory
 template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
-                           bool valid, int co_base, const f32x4* lp = nullptr) {
+                           bool valid, int co_base, const f32x4* lp = nullptr, float* lst = nullptr) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int C4o = (p.Cout + 3) >> 2;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
@@ -629,10 +629,103 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           }
         }
       }
+    } else if constexpr (X6 == 1) {
+      // x6 with a residual gradient and / or C = 192 (the cheng2020 k3 s1 kernels, 1 wave/SIMD): ONE pass over the
+      // saved (y, s) like the plain branch above.  g*s is parked in this wave's LDS slab lst (IT*16 floats per
+      // lane: the kernel's patch, idle after its main loop), 2x replaces g in the accumulators and t goes straight
+      // into its three bf16 planes; u = gamma'^T t runs in two halves of IT/2 output tiles (fragments a round
+      // ahead), so neither y, s nor a parked g*s is read twice from memory.  Same per-element ops as the fp32 form.
+      static_assert(!BF && (FX & ~FX_RES) == 0 && IT % 2 == 0, "x6 GDN-bwd epilogue: residual view, even IT");
+      const unsigned vo_ld = valid ? vo : 0x0FFFFFF0u;   // past the descriptor's range: loads return 0
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((FX & FX_RES) != 0) {
+        const Img SX(p.save_x, p.save_x ? img : 0, n), RS(p.res, p.res ? img : 0, n);   // absent: zero-size range
+        f32x4 rq[IT][4];
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) rq[it][g] = RS.ld(vo_ld, so(it * 8 + 2 * g));
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += rq[it][g][e];
+            if (p.save_x && valid)
+              SX.st(vo, so(it * 8 + 2 * g),
+                    f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      f32x4 yq[IT][4], sq[IT][4];
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          yq[it][g] = IX.ld(vo_ld, so(it * 8 + 2 * g));
+          sq[it][g] = IS.ld(vo_ld, so(it * 8 + 2 * g));
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 tq[IT][2][3];
+      float tw[8];
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sg = sq[it][g][e], xs = yq[it][g][e] / sg;
+            const float gx = acc[it][4 * g + e] * xs;
+            tw[4 * (g & 1) + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : gx / (2.0f * sg);
+            float gs = acc[it][4 * g + e] * sg;
+            float x2 = 2.0f * xs;
+            asm volatile("" : "+v"(gs), "+v"(x2));   // materialise (see the bf16 branch)
+            lst[((it * 4 + g) * 4 + e) * 64 + lane] = gs;
+            acc[it][4 * g + e] = x2;
+          }
+          if (g & 1) split3x8(tw, tq[it][g >> 1]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+      constexpr int H2 = IT / 2;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        f32x16 ux[H2];
+#pragma unroll
+        for (int j = 0; j < H2; ++j) ux[j] = f32x16{0};
+        bf16x8 ga[2][H2][3];
+        auto ldg = [&](bf16x8 (&a)[H2][3], int k) {
+#pragma unroll
+          for (int j = 0; j < H2; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              a[j][q] = ld_bf8(grs, lane * 16,
+                               ((((hb * H2 + j) * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+        };
+        ldg(ga[0], 0);
+#pragma unroll
+        for (int k = 0; k < 2 * IT; ++k) {
+          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < H2; ++j) ux[j] = mfma_x6(ga[k & 1][j], tq[k >> 1][k & 1], ux[j]);
+        }
+        if (valid) {
+#pragma unroll
+          for (int j = 0; j < H2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int jt = hb * H2 + j;
+              f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                v[e] = lst[((jt * 4 + g) * 4 + e) * 64 + lane] + acc[jt][4 * g + e] * ux[j][4 * g + e];
+              Y.st(vo, so(jt * 8 + 2 * g), v);
+            }
+        }
+      }
     } else {
-      // x6 (the cheng2020 k3 s1 kernels: residual gradient, C = 192): the same two-pass flow, u = gamma'^T t on x6
-      // operands in the wide form (t split into three planes as it is formed, every output tile at once)
-      static_assert(X6 != 2 && (X6 == 0 || (!BF && (FX & FX_T) == 0)), "x6 GDN-bwd epilogue: wide form, no t output");
+      static_assert(!X6, "x6 GDN-bwd epilogue: the single-pass branches above");
       if constexpr ((FX & FX_RES) != 0) {
         const Img SX(p.save_x, img, n), RS(p.res, img, n);
   #pragma unroll
@@ -668,10 +761,8 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       // the parity tests were pinned with.  bf16 path: GDN -0.5 g y s^2, IGDN 0.5 g y rcp(s)^2 (v_rcp_f32; the
       // epilogue was VALU-bound on division sequences), and t goes straight into its hi/lo B fragments
       // (register r = 4g+e is k-step r>>3, element r&7), no fp32 copy kept.
-      f32x16 tt[(BF || X6) ? 1 : IT];
+      f32x16 tt[BF ? 1 : IT];
       bf16x8 th[BF ? IT : 1][2], tl[BF ? IT : 1][2];
-      bf16x8 tq[X6 == 1 ? IT : 1][2][3];   // x6: t of k-step s (registers 8s..8s+7) as three bf16 planes
-      float tw[8];
       const Img ST((FX & FX_T) ? p.save_t : nullptr, img, n);
   #pragma unroll
       for (int it = 0; it < IT; ++it)
@@ -703,48 +794,20 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
               split_bf(t, hi, lo);
               th[it][g >> 1][4 * (g & 1) + e] = hi;
               tl[it][g >> 1][4 * (g & 1) + e] = lo;
-            } else if constexpr (X6 == 1) {
-              tw[4 * (g & 1) + e] = t;
             } else {
               tt[it][4 * g + e] = t;
             }
-          }
-          if constexpr (X6 == 1) {
-            if (g & 1) split3x8(tw, tq[it][g >> 1]);
           }
           if constexpr ((FX & FX_T) != 0) {
             if (valid) ST.st(vo, ss, tv);
           }
         }
-      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, X6 ? IT * IT * 6144 : IT * IT * 4096);
-      f32x16 ux[X6 == 1 ? IT : 1];
-      if constexpr (X6 == 1) {   // round k = (k-tile ct, k-step s) feeds every output tile; fragments a round ahead
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int jt = 0; jt < IT; ++jt) ux[jt] = f32x16{0};
-        bf16x8 ga[2][IT][3];
-        auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
-#pragma unroll
-          for (int jt = 0; jt < IT; ++jt)
-#pragma unroll
-            for (int q = 0; q < 3; ++q)
-              a[jt][q] = ld_bf8(grs, lane * 16, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
-        };
-        ldg(ga[0], 0);
-#pragma unroll
-        for (int k = 0; k < 2 * IT; ++k) {
-          if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int jt = 0; jt < IT; ++jt) ux[jt] = mfma_x6(ga[k & 1][jt], tq[k >> 1][k & 1], ux[jt]);
-        }
-      }
+      const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
   #pragma unroll
       for (int jt = 0; jt < IT; ++jt) {
         f32x16 uacc = f32x16{0};
-        if constexpr (X6 == 1) uacc = ux[jt];
   #pragma unroll
-        for (int ct = 0; ct < (X6 ? 0 : IT); ++ct) {
+        for (int ct = 0; ct < IT; ++ct) {
           if constexpr (BF) {
             const int o = (jt * IT + ct) * 4096;
   #pragma unroll
