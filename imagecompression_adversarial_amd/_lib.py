@@ -35,6 +35,9 @@ _SIGS = {
     "ica_pack_gdn_x6_size": [_i],
     "ica_pack_up3_bf16": [_p, _p, _i, _p],
     "ica_pack_up3_x6": [_p, _p, _i, _p],
+    "ica_pack_up3k3_x6_size": [_i],
+    "ica_pack_up3k3_x6": [_p, _p, _p, _i, _p],
+    "ica_conv_up3k3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p],
     "ica_conv_up3_x6": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_up3_bf16": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "ica_conv_ex": [_p, _p],
@@ -116,7 +119,7 @@ _SIGS = {
     "ica_mse_grad": [_p, _p, _p, _i, _i, _i, _f, _p],
 }
 _RESTYPES = {"ica_pack_conv_weight_size": _sz, "ica_pack_conv_weight_bf16_size": _sz,
-             "ica_pack_conv_weight_x6_size": _sz, "ica_pack_gdn_x6_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz,
+             "ica_pack_conv_weight_x6_size": _sz, "ica_pack_gdn_x6_size": _sz, "ica_pack_up3k3_x6_size": _sz, "ica_pack_up3_size": _sz, "ica_wgrad_ws_size": _sz,
              "ica_rans_encode": _l, "ica_ar_lds_bytes": _sz}
 
 

@@ -72,10 +72,11 @@ template <int KS, int IT, int CC, int EPI, bool BF>
 constexpr int conv_down_waves() { return (BF && CC == 4 && EPI == EPI_GDN) ? 4 : conv_min_blocks<KS, IT>(); }
 
 // X6O: fp32-accurate bf16x6 operands (fp32 activations split into three bf16 planes as the patch is staged, the
-// three-plane weight pack of ica_pack_conv_weight_x6, six MFMAs per 16-deep k step; the epilogue is the fp32 one with
-// the fp32 gamma' pack): the k3 s1 layers of cheng2020 on the x6 ceiling.  One block per CU (512 registers).
+// three-plane weight pack of ica_pack_conv_weight_x6, six MFMAs per 16-deep k step; x6 GDN epilogue GEMMs on the
+// ica_pack_gdn_x6 pack): the k3 s1 layers of cheng2020 on the x6 ceiling.  One block per CU (512 registers); two for
+// IT = 1 (g_s.7's 16 rho rows: 16 accumulators).
 template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false>
-__global__ __launch_bounds__(256, X6O ? 1 : (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
   constexpr int PT = down_pt<CC, BF>();
   constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
@@ -1742,6 +1743,8 @@ static int pick_epi_down_x6o(const ConvParams& p, int epi, int fx, hipStream_t s
 static int pick_down_x6o(const ConvParams& p, int it, int epi, int fx, hipStream_t st) {
   if (p.Cin < 16) return -4;
   switch (it) {
+    case 1:   // cheng2020 g_s.7, subpel_conv3x3(N, 3, 2): 16 rho rows, PixelShuffle store
+      return epi == EPI_BIAS && fx == FX_PS ? pick_tw_down_x6o<1, EPI_BIAS, FX_PS>(p, st) : -4;
     case 4: return pick_epi_down_x6o<4>(p, epi, fx, st);
     case 6: return pick_epi_down_x6o<6>(p, epi, fx, st);
     default: return -4;

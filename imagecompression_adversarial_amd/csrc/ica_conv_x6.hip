@@ -1403,6 +1403,160 @@ __global__ void pack_gdn_x6_kernel(const float* __restrict__ gp, __bf16* __restr
   dst[2 * total + i] = (__bf16)(r1 - (float)b);
 }
 
+// --------------------------------------------------------------------------------------------------------------
+// cheng2020 g_a.0 input gradient (ResidualBlockWithStride(3, N): conv1 = conv3x3(3, N, s2) and skip = conv1x1(3, N,
+// s2), both read the image): dx = conv1^T g1 + skip^T gs in ONE pass.  A 3-channel output is a poor MFMA row tile
+// (the two fp32 conv_up launches computed 32 rows for 3 and read their inputs separately: 6.7 ms at the config-3
+// shapes), so the kernel runs the Z-gather of conv_up3: Z = Wt^T [g1; gs] for every gradient pixel (rows 0-26:
+// (c, ky, kx) of conv1 over the g1 channels, rows 27-29: c of the skip over the gs channels; K = 2 Cg), on x6
+// operands, into LDS, then each output pixel sums its 1, 2 or 4 conv1 taps and (even pixels) the skip row.
+// Tile: UK_ZR = 16 gradient rows x 32 columns of Z (4 rows per wave), outputs for the first 15 x 31 of them (the
+// transposed k3 s2 conv reads rows a, a + 1 and columns b, b + 1 of g for output row 2a + 1 / column 2b + 1).
+// --------------------------------------------------------------------------------------------------------------
+constexpr int UK_ZR = 16, UK_R = UK_ZR - 1, UK_OW = 31, UK_NPX = UK_ZR * 32;
+
+// [plane][chunk][lane][e] (K = 2 Cg, chunk = 16 channels): lane (h, row) holds A[row][k = 16 chunk + 8 h + e]
+__global__ void pack_up3k3_x6_kernel(const float* __restrict__ w1, const float* __restrict__ ws, __bf16* __restrict__ dst,
+                                     int Cg, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int e = i % 8, lane = (i / 8) % 64, chunk = (int)(i / 512);
+  const int row = lane & 31, k = chunk * 16 + (lane >> 5) * 8 + e;
+  float v = 0.f;
+  if (row < 27 && k < Cg) v = w1[((long)k * 3 + row / 9) * 9 + row % 9];               // conv1 [Cg][3][3][3]
+  else if (row >= 27 && row < 30 && k >= Cg) v = ws[(long)(k - Cg) * 3 + (row - 27)];   // skip [Cg][3][1][1]
+  const __bf16 a = (__bf16)v;
+  const float r1 = v - (float)a;
+  const __bf16 b = (__bf16)r1;
+  dst[i] = a;
+  dst[total + i] = b;
+  dst[2 * total + i] = (__bf16)(r1 - (float)b);
+}
+
+__global__ __launch_bounds__(256, 2) void conv_up3k3_x6_kernel(const float* __restrict__ g1, const float* __restrict__ gs,
+                                                                const void* __restrict__ wp, float* __restrict__ dx,
+                                                                int Cg, int Hin, int Win, int Hout, int Wout) {
+  __shared__ float zs[32 * UK_NPX];
+  const int tiles_x = (Win + UK_OW - 1) / UK_OW, tiles_y = (Hin + UK_R - 1) / UK_R;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int n = bid / tiles_y;
+  const int a0 = ty * UK_R, b0 = tx * UK_OW;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Cg4 = Cg >> 2, nchg = Cg >> 4, nch = 2 * nchg;
+  const unsigned plane = (unsigned)Hin * Win;
+  const __amdgpu_buffer_rsrc_t r1 = uniform_rsrc(g1 + (size_t)n * Cg4 * plane * 4, (unsigned)(Cg4 * plane * 16));
+  const __amdgpu_buffer_rsrc_t r2 = uniform_rsrc(gs + (size_t)n * Cg4 * plane * 4, (unsigned)(Cg4 * plane * 16));
+  constexpr unsigned OOB = 0xFFFFFFF0u;
+  // Z tile k of this wave: gradient row a0 + wave + 4k, column b0 + j; the lane's quads 2h, 2h + 1 of each chunk
+  unsigned po[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int iy = a0 + wave + 4 * k, ix = b0 + j;
+    po[k] = iy < Hin && ix < Win ? ((unsigned)(2 * h) * plane + (unsigned)iy * Win + ix) * 16u : OOB;
+  }
+  const long pst = (long)nch * 64;   // fragments per plane
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(wp, (unsigned)(3 * pst * 16));
+  auto ldw = [&](bf16x8 (&a)[3], int ch) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] = ld_bf8(wr, lane * 16, (int)((q * pst + (long)ch * 64) * 16));
+  };
+  auto ldx = [&](f32x4 (&v)[4][2], int ch) {
+    const bool second = ch >= nchg;   // wave-uniform: chunks 0..nchg-1 read g1, the rest gs
+    const __amdgpu_buffer_rsrc_t r = second ? r2 : r1;
+    const unsigned co = (unsigned)(second ? ch - nchg : ch) * 4u * plane * 16u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = po[k] != OOB;
+      v[k][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? po[k] + co : OOB, 0, 0));
+      v[k][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? po[k] + co + plane * 16u : OOB,
+                                                                                 0, 0));
+    }
+  };
+  f32x16 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = f32x16{0};
+  auto compute = [&](const bf16x8 (&a)[3], const f32x4 (&v)[4][2]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x[8] = {v[k][0][0], v[k][0][1], v[k][0][2], v[k][0][3], v[k][1][0], v[k][1][1], v[k][1][2], v[k][1][3]};
+      bf16x8 b[3];
+      split3x8(x, b);
+      acc[k] = mfma_x6(a, b, acc[k]);
+    }
+  };
+  // chunk ch + 1's weights and gradients in flight during chunk ch's MFMAs (ping-pong; nch is even)
+  bf16x8 wa[3], wb[3];
+  f32x4 xa[4][2], xb[4][2];
+  ldw(wa, 0);
+  ldx(xa, 0);
+#pragma unroll 1
+  for (int ch = 0; ch < nch; ch += 2) {
+    ldw(wb, ch + 1);
+    ldx(xb, ch + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(wa, xa);
+    if (ch + 2 < nch) {
+      ldw(wa, ch + 2);
+      ldx(xa, ch + 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    compute(wb, xb);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = acc_row(r, h);
+      if (row < 30) zs[row * UK_NPX + (wave + 4 * k) * 32 + j] = acc[k][r];
+    }
+  __syncthreads();
+  // gather: thread -> output row 2 al + py, columns 2 bl, 2 bl + 1 (32 contiguous bytes per thread)
+  for (int e = threadIdx.x; e < 2 * UK_R * UK_OW; e += 256) {
+    const int yl = e / UK_OW, bl = e - yl * UK_OW;
+    const int al = yl >> 1, py = yl & 1;
+    const int a = a0 + al, b = b0 + bl;
+    if (a >= Hin || b >= Win) continue;
+    f32x4 o[2];
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      float s[3] = {0.f, 0.f, 0.f};
+      // taps of output parity (py, px): ky = 1 (row a) for py = 0; ky = 0 (row a + 1), 2 (row a) for py = 1
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        if ((ky & 1) == py) continue;   // ky = 1 <-> py = 0
+        const int dr = (py + 1 - ky) >> 1;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          if ((kx & 1) == px) continue;
+          const int dc = (px + 1 - kx) >> 1;
+          const int q = (al + dr) * 32 + bl + dc;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) s[c] += zs[(c * 9 + ky * 3 + kx) * UK_NPX + q];
+        }
+      }
+      if (py == 0 && px == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) s[c] += zs[(27 + c) * UK_NPX + al * 32 + bl];
+      }
+      o[px] = f32x4{s[0], s[1], s[2], 0.f};
+    }
+    const int y = 2 * a + py, x = 2 * b;
+    if (y < Hout) {
+      float* d = dx + (((size_t)n * Hout + y) * Wout + x) * 4;
+      if (x + 1 < Wout) {
+        st4(d, o[0]);
+        st4(d + 4, o[1]);
+      } else if (x < Wout) {
+        st4(d, o[0]);
+      }
+    }
+  }
+}
+
 template <int IT, int EPI, int PT>
 int launch_down_x6_pt(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Wout + XD_TW - 1) / XD_TW) * ((p.Hout + xd_th<PT>() - 1) / xd_th<PT>()) * p.N;
@@ -1647,6 +1801,30 @@ int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, lon
                reinterpret_cast<__bf16*>(dst) + 3 * total, O, C, so, sc, it, t2);
     ICA_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+size_t ica_pack_up3k3_x6_size(int Cg) { return (size_t)3 * (2 * Cg / 16) * 64 * 16; }
+
+// the fused g_a.0 input-gradient pack: conv1 [Cg][3][3][3] and skip [Cg][3][1][1] weights -> three bf16 planes
+int ica_pack_up3k3_x6(const float* w1, const float* ws, void* dst, int Cg, hipStream_t st) {
+  if (Cg <= 0 || Cg % 16 != 0) return -2;
+  const long total = (long)(2 * Cg / 16) * 512;
+  ICA_LAUNCH(pack_up3k3_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w1, ws, reinterpret_cast<__bf16*>(dst),
+             Cg, total);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+// dx [N][1][Hout][Wout][4] = conv3x3_s2^T(g1) + conv1x1_s2^T(gs); g1, gs [N][Cg/4][Hin][Win][4] row-major,
+// Hin = ceil(Hout / 2), Win = ceil(Wout / 2)
+int ica_conv_up3k3_x6(const float* g1, const float* gs, const void* wp, float* dx, int N, int Cg, int Hin, int Win,
+                      int Hout, int Wout, hipStream_t st) {
+  if (Cg <= 0 || Cg % 16 != 0 || N <= 0) return -2;
+  if (Hin != (Hout + 1) / 2 || Win != (Wout + 1) / 2) return -3;
+  const long blocks = (long)((Win + UK_OW - 1) / UK_OW) * ((Hin + UK_R - 1) / UK_R) * N;
+  ICA_LAUNCH(conv_up3k3_x6_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g1, gs, wp, dx, Cg, Hin, Win, Hout, Wout);
+  ICA_CHECK_LAUNCH();
   return 0;
 }
 

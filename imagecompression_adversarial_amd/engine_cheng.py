@@ -61,6 +61,7 @@ def _rho_weight(w, b, C):
 
 
 X6_IT = (4, 6)   # row tiles of the x6 k3 s1 conv_down instantiations (ica_conv.hip pick_down_x6o)
+X6_IT_PS = (1, 4, 6)   # ... and of the subpel forwards (IT = 1: g_s.7's 16 rho rows, bias + PixelShuffle only)
 
 
 class Conv3:
@@ -128,7 +129,7 @@ class Subpel:
         self.fwd = K.pack_conv(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, 16, it=self.it)
         # x6 forward (PixelShuffle store) and input gradient (PixelUnshuffle fill, the flipped weight)
         self.fwd6 = (K.pack_conv_x6(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, self.it)
-                     if x6 and self.Cin >= 16 and self.it in X6_IT else None)
+                     if x6 and self.Cin >= 16 and self.it in X6_IT_PS else None)
         self.it_b = _it(self.Cin)
         self.bwd = None if fwd_only else K.pack_conv(wr, self.Cin, self.R, 3, 9, self.Cin * 9, K.ORDER_DOWN, 16,
                                                      flip=True, it=self.it_b)
@@ -175,9 +176,17 @@ class ChengAnalysis:
                 self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6),
                                     Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6)))
         self.last = Conv3(sd[_k(prefix, "6.weight")], sd[_k(prefix, "6.bias")], 2)
+        # x6: the image-side block's two input gradients (conv1 k3 s2 and skip k1 s2 into 3 channels) as one fused
+        # Z-gather launch (ica_conv_up3k3_x6) instead of two 32-row fp32 conv_up tiles computing 3 rows each
+        w1, wsk = sd[_k(prefix, "0.conv1.weight")], sd[_k(prefix, "0.skip.weight")]
+        self.rgb6 = (K.pack_up3k3_x6(w1, wsk) if x6 and w1.shape[1] == 3 and w1.shape[0] % 16 == 0
+                     and tuple(wsk.shape[1:]) == (3, 1, 1) else None)
+        self._in_hw = None
 
     def forward(self, x4, save=False):
         h, saved = x4, []
+        if save:
+            self._in_hw = (x4.shape[2], x4.shape[3])
         for i, blk in enumerate(self.blocks):
             t = f"{self.tag}.{i}"
             if blk[0] == "rbs":
@@ -217,6 +226,11 @@ class ChengAnalysis:
                 _, c1, c2, sk, gd = blk
                 a1 = sv[0]
                 gc1 = c2.dgrad(g, K.EPI_LRELU_BWD, saved=(a1, None), tag=f"{t}.conv2.dgrad")
+                hw = self._in_hw
+                if (i == 0 and self.rgb6 is not None and hw is not None and (hw[0] + 1) // 2 == gc1.shape[2]
+                        and (hw[1] + 1) // 2 == gc1.shape[3]):
+                    g = K.conv_up3k3_x6(gc1, g_sum, self.rgb6, hw[0], hw[1], tag=f"{t}.conv1+skip.dgrad")
+                    continue
                 r = sk.dgrad(g_sum, tag=f"{t}.skip.dgrad")
                 g = c1.dgrad(gc1, K.EPI_BIAS, res=r, tag=f"{t}.conv1.dgrad")
                 del r

@@ -529,6 +529,37 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
     return y
 
 
+def pack_up3k3_x6(w1: torch.Tensor, ws: torch.Tensor) -> torch.Tensor:
+    """Fragments of conv_up3k3_x6 (three bf16 planes) from the conv1 [Cg][3][3][3] and skip [Cg][3][1][1] weights of
+    cheng2020's g_a.0 (ResidualBlockWithStride(3, N))."""
+    w1, ws = w1.detach().contiguous(), ws.detach().contiguous()
+    _dev_check(w1, "weight")
+    _dev_check(ws, "weight")
+    Cg = w1.shape[0]
+    if tuple(w1.shape) != (Cg, 3, 3, 3) or tuple(ws.shape) != (Cg, 3, 1, 1):
+        raise RuntimeError("pack_up3k3_x6: conv1 [Cg][3][3][3] and skip [Cg][3][1][1] weights")
+    dst = torch.empty(int(lib().ica_pack_up3k3_x6_size(Cg)) // 2, dtype=torch.bfloat16, device=w1.device)
+    call("ica_pack_up3k3_x6", ptr(w1), ptr(ws), ptr(dst), Cg, stream())
+    return dst
+
+
+def conv_up3k3_x6(g1: torch.Tensor, gs: torch.Tensor, wp: torch.Tensor, Hout: int, Wout: int, tag=None):
+    """dx = conv3x3_s2^T(g1) + conv1x1_s2^T(gs) for a 3-channel input (x6 operands, one pass; ica_conv_up3k3_x6).
+    g1, gs: nChw4c [N][Cg/4][H][W][4] row-major; returns dx [N][1][Hout][Wout][4]."""
+    for t, nm in ((g1, "g1"), (gs, "gs")):
+        _dev_check(t, nm)
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise RuntimeError(f"conv_up3k3_x6: {nm} must be contiguous fp32 nChw4c")
+    if g1.shape != gs.shape:
+        raise RuntimeError("conv_up3k3_x6: g1 and gs shapes differ")
+    N, C4, H, W, _ = g1.shape
+    dx = empty_nc4(N, 3, Hout, Wout, g1.device)
+    ev = _ev_begin(tag, N)
+    call("ica_conv_up3k3_x6", ptr(g1), ptr(gs), ptr(wp), ptr(dx), N, 4 * C4, H, W, Hout, Wout, stream())
+    _ev_end(ev, 2.0 * 4 * C4 * 3 * (9 + 1) * N * H * W)
+    return dx
+
+
 # --------------------------------------------------------------------------- #
 # Reductions / elementwise
 # --------------------------------------------------------------------------- #

@@ -91,6 +91,15 @@ size_t ica_pack_conv_weight_bf16_size(int O, int C, int KS, int it);
 int ica_pack_up3_x6(const float* w, void* dst, int Cin, hipStream_t stream);
 int ica_conv_up3_x6(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
                     int layout, hipStream_t stream);
+/* cheng2020 g_a.0 input gradient, fused (replaces the backward of compressai ResidualBlockWithStride(3, N)'s conv1 =
+ * conv3x3(3, N, stride 2) and skip = conv1x1(3, N, stride 2), reference anchors/model.py:76-77 -> cheng2020_anchor):
+ * dx [N][1][Hout][Wout][4] = conv3x3_s2^T(g1) + conv1x1_s2^T(gs), g1 / gs [N][Cg/4][Hin][Win][4] row-major, Hin =
+ * ceil(Hout / 2), Win = ceil(Wout / 2), Cg % 16 == 0; x6 operands.  Weights: conv1 [Cg][3][3][3], skip [Cg][3][1][1]
+ * -> ica_pack_up3k3_x6 (ica_pack_up3k3_x6_size(Cg) bytes). */
+int ica_pack_up3k3_x6(const float* w1, const float* ws, void* dst, int Cg, hipStream_t stream);
+size_t ica_pack_up3k3_x6_size(int Cg);
+int ica_conv_up3k3_x6(const float* g1, const float* gs, const void* wp, float* dx, int N, int Cg, int Hin, int Win,
+                      int Hout, int Wout, hipStream_t stream);
 int ica_pack_up3_bf16(const float* w, void* dst, int Cin, hipStream_t stream);
 int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bias, int N, int Cin, int Hin, int Win,
                       int layout, hipStream_t stream);

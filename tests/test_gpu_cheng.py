@@ -60,6 +60,27 @@ def test_conv_modes_vs_torch(K, Cin, Cout, KS, S, H, W):
         assert rel_err(gx, xr.grad) < 1e-4
 
 
+@pytest.mark.parametrize("H,W,Cg", [(64, 64, 192), (66, 94, 192), (63, 97, 128), (30, 62, 16)])
+def test_rgb_block_input_gradient_fused_x6(K, H, W, Cg):
+    """cheng2020 g_a.0 (ResidualBlockWithStride(3, N)): the fused x6 input gradient conv3x3_s2^T(g1) + conv1x1_s2^T(gs)
+    (ica_conv_up3k3_x6) against float64 autograd of the two forward convs, at the fp32 tolerance; odd image sides
+    (Hin = ceil(H / 2)) and tiles cut by the image edge (15 x 31 gradient pixels per block)."""
+    w1 = rnd((Cg, 3, 3, 3), 11) / 27 ** 0.5
+    ws = rnd((Cg, 3, 1, 1), 12) / 3 ** 0.5
+    Hc, Wc = (H + 1) // 2, (W + 1) // 2
+    g1, gs = rnd((2, Cg, Hc, Wc), 13), rnd((2, Cg, Hc, Wc), 14)
+    x = torch.zeros((2, 3, H, W), dtype=torch.float64, requires_grad=True)
+    y1 = F.conv2d(x, w1.double(), stride=2, padding=1)
+    ys = F.conv2d(x, ws.double(), stride=2)
+    assert y1.shape[2:] == (Hc, Wc) and ys.shape[2:] == (Hc, Wc)
+    ((y1 * g1.double()).sum() + (ys * gs.double()).sum()).backward()
+    wp = K.pack_up3k3_x6(w1.to(DEV), ws.to(DEV))
+    dx = K.conv_up3k3_x6(K.to_nc4(g1.to(DEV)), K.to_nc4(gs.to(DEV)), wp, H, W)
+    got = K.from_nc4(dx, 3).cpu().double()
+    assert rel_err(got, x.grad) < 2e-6
+    assert float(dx[..., 3].abs().max()) == 0.0   # the padding channel of the 3-channel quad
+
+
 def test_residual_saves_and_lrelu_masks(K):
     """RB pieces: y = lrelu(conv(a)) + x with the activation saved; dgrad with the input masked by
     lrelu'(a2) in the LDS fill and the output masked by lrelu'(a1) in the epilogue; dgrad + residual."""
