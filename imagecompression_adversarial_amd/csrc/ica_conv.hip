@@ -906,7 +906,7 @@ ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], 
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-    conv_epilogue<IT, EPI, FX, BF, 0, BF>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lp);
+    conv_epilogue<IT, EPI, FX, BF, 0, BF, false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lp);
   }
 }
 
