@@ -759,10 +759,11 @@ constexpr int xu_plane() { return (xu_th<PT>() + 2) * XU_PC; }   // 180 px (PT =
 template <int CG, int PT>
 constexpr int xu_lds_bytes() { return 3 * (CG / 8) * xu_plane<PT>() * 16; }
 
-template <int PY, int PX, int IT, int CG, int PT>
+// KS = 3 (cheng2020's conv3x3 stride-2 input gradients, pad 1): the same decomposition, 1 / 2 / 2 / 4 taps per class
+template <int PY, int PX, int IT, int CG, int PT, int KS = 5>
 ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch, int grp, long ps,
                               f32x16 (&acc)[PT][IT]) {
-  constexpr int KS = 5, PAD = 2, XU_PLANE = xu_plane<PT>();
+  constexpr int PAD = KS / 2, XU_PLANE = xu_plane<PT>();
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
   constexpr int NCG = CG / 16;   // 16-channel chunks per LDS group
@@ -822,7 +823,7 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
   if (u < total) step(fa, fb, ba, bb, u);
 }
 
-template <int IT, int EPI, int CG, int PT = X6_PT>
+template <int IT, int EPI, int CG, int PT = X6_PT, int KS = 5, int FX = 0>
 __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long ps) {
   constexpr int NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
   extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
@@ -886,7 +887,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
       for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
     for (int grp = 0; grp < ngrp; ++grp) {
       if (refill) fill(grp);
-      conv_up_x6_class<PY, PX, IT, CG, PT>(p, patch, jt, cb, nch, grp, ps, acc);
+      conv_up_x6_class<PY, PX, IT, CG, PT, KS>(p, patch, jt, cb, nch, grp, ps, acc);
     }
     if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
       const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
@@ -896,7 +897,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
         const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-        conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
+        conv_epilogue<IT, EPI, FX, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
       }
     }
   };
@@ -1690,6 +1691,45 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
   return launch_up_x6_pt<IT, EPI, CG, X6_PT>(p, st);
 }
 
+// the k3 s2 input gradients of cheng2020's stride-2 residual blocks (conv_ex kind 1, x6): bias (+ residual) epilogue
+template <int IT, int FX, int CG, int PT>
+int launch_up3s2_x6_pt(const ConvParams& p, hipStream_t st) {
+  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<PT>() - 1) / xu_th<PT>()) * p.N;
+  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long ps = (long)ncb * 9 * (p.Cin / 16) * IT * 64;
+  constexpr size_t lds = xu_lds_bytes<CG, PT>();
+  static_assert(lds <= 160 * 1024, "conv_up_x6 channel group exceeds LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6_kernel<IT, EPI_BIAS, CG, PT, 3, FX>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  ICA_LAUNCH((conv_up_x6_kernel<IT, EPI_BIAS, CG, PT, 3, FX>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+template <int IT, int FX, int CG>
+int launch_up3s2_x6(const ConvParams& p, hipStream_t st) {
+  const long ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
+  const long b2 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N * ncb;
+  const long b1 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<1>() - 1) / xu_th<1>()) * p.N * ncb;
+  if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) return launch_up3s2_x6_pt<IT, FX, CG, 1>(p, st);
+  return launch_up3s2_x6_pt<IT, FX, CG, 2>(p, st);
+}
+static int pick_up3s2_x6(const ConvParams& p, int it, int epi, int fx, hipStream_t st) {
+  if (epi != EPI_BIAS || (fx != 0 && fx != FX_RES) || p.Cout % 32 != 0) return -4;
+  if (p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win || (p.pl & (PL_IN | PL_OUT))) return -2;
+  const bool res = fx == FX_RES;
+  // Cin = 192: the whole channel range in LDS at PT = 1 (124 KB), one fill per block -- in 64-channel groups each
+  // class re-staged a group for 1-4 taps (g_a.2.conv1.dgrad 4.33 ms at the config-3 shapes)
+  if (it == 6 && p.Cin == 192)
+    return res ? launch_up3s2_x6_pt<6, FX_RES, 192, 1>(p, st) : launch_up3s2_x6_pt<6, 0, 192, 1>(p, st);
+  if (it == 4 && p.Cin == 128)
+    return res ? launch_up3s2_x6<4, FX_RES, 128>(p, st) : launch_up3s2_x6<4, 0, 128>(p, st);
+  return -3;
+}
+
 template <int IT, int EPI>
 int launch_up_small_x6(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Win + 15) / 16) * ((p.Hin + XSU_TH - 1) / XSU_TH) * p.N;
@@ -1726,6 +1766,7 @@ int pick_up_x6(const ConvParams& p, hipStream_t st) {
 // bmshj2018 transforms.  Returns -4 / -3 / -2 / -5 for shapes / epilogues without an x6 kernel: nothing falls back
 // here; hip_ops.x6_ok restates this coverage so that PackedConv keeps the fp32 pack for such layers.
 int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, int epi, int fx, hipStream_t st) {
+  if (kind == 1 && KS == 3 && S == 2) return pick_up3s2_x6(p, it, epi, fx, st);
   if (KS != 5 || S != 2 || fx != 0) return -4;
   if (p.Cout % 32 != 0) return -4;
   if (kind == 0) {

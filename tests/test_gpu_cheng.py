@@ -60,6 +60,26 @@ def test_conv_modes_vs_torch(K, Cin, Cout, KS, S, H, W):
         assert rel_err(gx, xr.grad) < 1e-4
 
 
+@pytest.mark.parametrize("H,W,res", [(64, 96, True), (32, 48, False), (96, 160, True)])
+def test_stride2_conv_input_gradient_x6(K, H, W, res):
+    """The x6 input gradient of the stride-2 conv3x3 (cheng2020 g_a.2 / g_a.4 conv1: conv_up_x6 with KS = 3, IT = 6, a
+    64-channel LDS group, bias + residual epilogue) against float64 autograd, at the fp32 tolerance."""
+    from imagecompression_adversarial_amd.engine_cheng import Conv3
+    C = 192
+    w = rnd((C, C, 3, 3), 21) / (C * 9) ** 0.5
+    b = rnd((C,), 22) * 0.1
+    c = Conv3(w.to(DEV), b.to(DEV), 2, x6=True)
+    assert c.bwd6 is not None
+    g = rnd((2, C, H // 2, W // 2), 23)
+    r = rnd((2, C, H, W), 24)
+    x = torch.zeros((2, C, H, W), dtype=torch.float64, requires_grad=True)
+    F.conv2d(x, w.double(), b.double(), stride=2, padding=1).backward(g.double())
+    ref = x.grad + (r.double() if res else 0.0)
+    kw = {"res": K.to_nc4(r.to(DEV))} if res else {}
+    got = K.from_nc4(c.dgrad(K.to_nc4(g.to(DEV)), **kw), C).cpu().double()
+    assert rel_err(got, ref) < 2e-6
+
+
 @pytest.mark.parametrize("H,W,Cg", [(64, 64, 192), (66, 94, 192), (63, 97, 128), (30, 62, 16)])
 def test_rgb_block_input_gradient_fused_x6(K, H, W, Cg):
     """cheng2020 g_a.0 (ResidualBlockWithStride(3, N)): the fused x6 input gradient conv3x3_s2^T(g1) + conv1x1_s2^T(gs)
