@@ -81,6 +81,38 @@ def kinks(P64, x64, rel=1e-6):
     return out
 
 
+def preact(P64, x64, call):
+    """The float64 input of leaky-ReLU call `call` of cheng_g_s(cheng_g_a(x)) (the order kinks() numbers them)."""
+    from oracle import codec as oc
+    seen = []
+    orig = oc.lrelu
+
+    def rec(a):
+        if len(seen) == call:
+            seen.append(a.detach().clone())
+        else:
+            seen.append(None)
+        return orig(a)
+
+    oc.lrelu = rec
+    try:
+        with torch.no_grad():
+            oc.cheng_g_s(P64, oc.cheng_g_a(P64, x64))
+    finally:
+        oc.lrelu = orig
+    return seen[call]
+
+
+def lrelu_slots(kern):
+    """Leaky-ReLU call index -> (transform, block, slot of the engine's saved tuple) for engine_cheng.ChengKernels:
+    slot 0 = a1 (conv1 / subpel output), 1 = a2 (a residual block's conv2 output before the residual add)."""
+    slots = []
+    for side, tr in (("g_a", kern.ga), ("g_s", kern.gs)):
+        for i, blk in enumerate(tr.blocks):
+            slots += [(side, i, 0), (side, i, 1)] if blk[0] == "rb" else [(side, i, 0)]
+    return slots
+
+
 def transforms_flipped(P64, x, flips=()):
     """cheng_g_s(cheng_g_a(x)) in float64 with the leaky ReLUs of the kinks in flips = [(call index, flat
     element)] taking their other branch (value and slope)."""

@@ -309,7 +309,7 @@ def kink_of(cheng6, cheng6x6):
     """Per path, the leaky-ReLU kink (tests/f64_replay.kinks) its forward puts on the other side than float64 on the
     seed-34 input, found from the input gradient under a random output gradient: per image, a list of kinks."""
     from imagecompression_adversarial_amd import hip_ops as K
-    from tests.f64_replay import match_kinks
+    from tests.f64_replay import lrelu_slots, match_kinks, preact
     out = {}
     x = rnd((2, 3, 64, 64), 34, 0.0, 1.0)
     gout = rnd((2, 3, 64, 64), 31).double()
@@ -318,9 +318,24 @@ def kink_of(cheng6, cheng6x6):
         xh4, ss = kern.g_s(y4, save=True)
         gx4 = kern.g_a_backward(kern.g_s_backward(K.to_nc4(gout.float().to(DEV)), ss), sa)
         P64 = {k: v.double() for k, v in P.items()}
-        out[path] = match_kinks(P64, x.double(), gout, K.from_nc4(gx4, 3))
-        print(f"{path}: kinks {out[path][0]}, input gradient error {out[path][1]:.2e}")
+        flips, err = match_kinks(P64, x.double(), gout, K.from_nc4(gx4, 3))
+        # each chosen flip confirmed on the path's own forward: its saved leaky-ReLU output at that element (same
+        # sign as its pre-activation) sits on the other side of zero than the float64 pre-activation
+        slots = lrelu_slots(kern)
+        crossed = []
+        for b, fl in enumerate(flips):
+            for c, e in fl:
+                side, i, slot = slots[c]
+                t = (sa if side == "g_a" else ss)[i][slot]
+                v = float(K.from_nc4(t, t.shape[1] * 4)[b].flatten()[e])
+                a64 = float(preact(P64, x[b:b + 1].double(), c).flatten()[e])
+                crossed.append((b, c, e, v, a64, (v > 0) != (a64 > 0)))
+        out[path] = (flips, err, crossed)
+        print(f"{path}: kinks {flips}, input gradient error {err:.2e}, path vs float64 at the flips {crossed}")
     return out
+
+
+KINKS_SEED34 = {"fp32": [[], [(19, 145950)]], "x6": [[], [(19, 145950)]]}
 
 
 @pytest.mark.parametrize("path", ["fp32", "x6"])
@@ -333,8 +348,12 @@ def test_cheng_input_gradient_vs_float64_kinks(kink_of, path):
     gamma' GEMMs in the k3 epilogues) x6 flipped two kinks (error 1.1e-4 unmatched), since round 4 (x6 epilogue
     GEMMs) the same single kink as the fp32 path (2.8e-6 matched, fp32 2.5e-6); scripts/cheng_x6_layer_diag.py shows
     the error switching on and off as single layers change operand path: a discontinuity, not accumulated error."""
-    flips, err = kink_of[path]
+    flips, err, crossed = kink_of[path]
     assert err <= 2e-5, (flips, err)
+    # every flip the match chose is a real crossing of the path's forward (not a fit of the reference)
+    assert all(c[-1] for c in crossed), crossed
+    # pinned flip sets (round 4 kernels): a kernel change that moves them shows up here
+    assert flips == KINKS_SEED34[path], flips
 
 
 @pytest.mark.parametrize("path", ["fp32", "x6"])
