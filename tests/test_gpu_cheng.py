@@ -360,7 +360,7 @@ def test_cheng_input_gradient_vs_float64_kinks(kink_of, path):
 def test_cheng_attack_divergence_vs_float64(cheng6, cheng6x6, kink_of, path, monkeypatch):
     """Seed 34, 4 steps, against the float64 replay of the oracle attack (tests/f64_replay.py) whose network step
     takes the path's kinks at step 0 (test above): every branch kept, every noise element within 1e-3 of the noise
-    max (measured: fp32 6.3e-4, x6 5.2e-4; the fp32 oracle itself, kinks unmatched: 7 beyond 1e-3, max 4.7e-3,
+    max (measured: fp32 6.3e-4, x6 2.6e-4; the fp32 oracle itself, kinks unmatched: 7 beyond 1e-3, max 4.7e-3,
     tests/test_cpu_cheng_conditioning.py).
     Without its kink the round-3 x6 trajectory left float64 by 6.5e-2 on 135 elements: the kink is taken at step 0 (noise
     0, the input of the test above; steps 1-2 take the cheap branch, step 3 the network again at lr 3.6e-4), and
