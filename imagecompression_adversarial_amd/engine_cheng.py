@@ -144,7 +144,8 @@ class Subpel:
                      if x6 and not fwd_only and self.R >= 16 and self.it_b in X6_IT else None)
 
     def forward(self, x4, epi=K.EPI_BIAS, **kw):
-        if self.fwd6 is not None and _x6_ok(kw):
+        # x6 at IT = 1 (g_s.7's 16 rho rows) is built for the bias epilogue only (ica_conv.hip pick_down_x6o)
+        if self.fwd6 is not None and _x6_ok(kw) and (self.it != 1 or epi == K.EPI_BIAS):
             return K.conv_ex(x4, self.Cin, self.fwd6, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,
                              alg_rows=4 * self.C, prec=K.PREC_X6, **kw)
         return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,

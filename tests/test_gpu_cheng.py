@@ -127,13 +127,18 @@ def test_residual_saves_and_lrelu_masks(K):
     assert rel_err(K.from_nc4(out, C).cpu(), F.conv_transpose2d(g, w, padding=1) + r) < 1e-4
 
 
-@pytest.mark.parametrize("Cin,C,H,W", [(192, 192, 8, 12), (192, 3, 16, 16), (288, 288, 4, 6)])
-def test_subpel_shuffle_vs_torch(K, Cin, C, H, W):
+@pytest.mark.parametrize("x6", [False, True])
+@pytest.mark.parametrize("Cin,C,H,W", [(192, 192, 8, 12), (192, 3, 16, 16), (288, 288, 4, 6), (192, 3, 16, 64)])
+def test_subpel_shuffle_vs_torch(K, Cin, C, H, W, x6):
+    """Subpel forward (PixelShuffle store) and input gradient (PixelUnshuffle fill), fp32 or x6 operands (x6 at
+    C = 3 is g_s.7's IT = 1 launch: bias epilogue on x6, the leaky-ReLU one on the fp32 pack)."""
     from imagecompression_adversarial_amd.engine_cheng import Subpel
     w = rnd((4 * C, Cin, 3, 3), 13) / (Cin * 9) ** 0.5
     b = rnd((4 * C,), 14) * 0.1
     x = rnd((2, Cin, H, W), 15)
-    sp = Subpel(w.to(DEV), b.to(DEV))
+    sp = Subpel(w.to(DEV), b.to(DEV), x6=x6)
+    if x6 and Cin != 288:
+        assert sp.fwd6 is not None
     ref = F.pixel_shuffle(F.conv2d(x, w, b, padding=1), 2)
     y = K.from_nc4(sp.forward(K.to_nc4(x.to(DEV)), K.EPI_BIAS), C).cpu()
     assert rel_err(y, ref) < 1e-4
@@ -147,10 +152,12 @@ def test_subpel_shuffle_vs_torch(K, Cin, C, H, W):
     assert rel_err(gx, xr.grad + r) < 1e-4
 
 
+@pytest.mark.parametrize("x6", [False, True])
 @pytest.mark.parametrize("inverse", [False, True])
-def test_gdn_residual_fwd_bwd(K, inverse):
+def test_gdn_residual_fwd_bwd(K, inverse, x6):
     """conv3x3 -> (I)GDN + r with y_gdn / s saved; backward with the upstream residual gradient added first
-    and the summed gradient saved (6-tile, C = 192)."""
+    and the summed gradient saved (6-tile, C = 192).  x6: the x6 normaliser / u GEMMs and the single-pass
+    backward with g*s parked in LDS (ica_conv_epi.h, X6 == 1 residual branch)."""
     from imagecompression_adversarial_amd.engine_cheng import Conv3
     C, H, W = 192, 8, 32
     P = oc.perturb_params({"t.beta": oc.gdn_init(C)[0], "t.gamma": oc.gdn_init(C)[1]}, seed=3)
@@ -158,7 +165,8 @@ def test_gdn_residual_fwd_bwd(K, inverse):
     w = rnd((C, C, 3, 3), 18) / (C * 9) ** 0.5
     b = rnd((C,), 19) * 0.1
     a, r = rnd((1, C, H, W), 20), rnd((1, C, H, W), 21)
-    c = Conv3(w.to(DEV), b.to(DEV), 1)
+    c = Conv3(w.to(DEV), b.to(DEV), 1, x6=x6)
+    assert (c.fwd6 is not None and c.bwd6 is not None) == x6
     gd = K.PackedGDN(beta.to(DEV), gamma.to(DEV))
     a4 = K.to_nc4(a.to(DEV))
     yg, s = torch.empty_like(a4), torch.empty_like(a4)
