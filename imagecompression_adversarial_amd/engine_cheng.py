@@ -188,12 +188,9 @@ class ChengAnalysis:
         w1, wsk = sd[_k(prefix, "0.conv1.weight")], sd[_k(prefix, "0.skip.weight")]
         self.rgb6 = (K.pack_up3k3_x6(w1, wsk) if x6 and w1.shape[1] == 3 and w1.shape[0] % 16 == 0
                      and tuple(wsk.shape[1:]) == (3, 1, 1) else None)
-        self._in_hw = None
 
     def forward(self, x4, save=False):
         h, saved = x4, []
-        if save:
-            self._in_hw = (x4.shape[2], x4.shape[3])
         for i, blk in enumerate(self.blocks):
             t = f"{self.tag}.{i}"
             if blk[0] == "rbs":
@@ -204,6 +201,8 @@ class ChengAnalysis:
                 s = torch.empty_like(r) if save else None
                 h = c2.forward(a1, K.EPI_GDN, gdn=gd, res=r, save_x=yg, save_s=s, tag=f"{t}.conv2.fwd")
                 del r
+                if save and i == 0:
+                    a1._ica_in_hw = (x4.shape[2], x4.shape[3])   # the image size, for the fused input gradient
                 saved.append((a1, yg, s) if save else None)
             else:
                 _, c1, c2 = blk
@@ -233,7 +232,7 @@ class ChengAnalysis:
                 _, c1, c2, sk, gd = blk
                 a1 = sv[0]
                 gc1 = c2.dgrad(g, K.EPI_LRELU_BWD, saved=(a1, None), tag=f"{t}.conv2.dgrad")
-                hw = self._in_hw
+                hw = getattr(a1, "_ica_in_hw", None)
                 if (i == 0 and self.rgb6 is not None and hw is not None and (hw[0] + 1) // 2 == gc1.shape[2]
                         and (hw[1] + 1) // 2 == gc1.shape[3]):
                     g = K.conv_up3k3_x6(gc1, g_sum, self.rgb6, hw[0], hw[1], tag=f"{t}.conv1+skip.dgrad")
@@ -283,6 +282,8 @@ class ChengSynthesis:
                 s = torch.empty_like(r) if save else None
                 h = cv.forward(a1, K.EPI_IGDN, gdn=gd, res=r, save_x=yg, save_s=s, tag=f"{t}.conv.fwd")
                 del r
+                if save and i == 0:
+                    a1._ica_in_hw = (x4.shape[2], x4.shape[3])   # the image size, for the fused input gradient
                 saved.append((a1, yg, s) if save else None)
         xh = self.last.forward(h, K.EPI_BIAS, tag=f"{self.tag}.7.fwd")
         return xh, saved

@@ -283,7 +283,13 @@ def test_cheng_x6_transforms_fwd_dgrad_vs_oracle(K, cheng6x6):
     gout = rnd(xhr.shape, 31)
     xhr.backward(gout)
     gy4 = kern.g_s_backward(K.to_nc4(gout.to(DEV)), ss)
-    gx4 = kern.g_a_backward(gy4, sa)
+    K.EVENT_HOOK = {}   # which launches ran: the fused image-side input gradient, not the two fp32 conv_ups
+    try:
+        gx4 = kern.g_a_backward(gy4, sa)
+        ran = set(K.EVENT_HOOK)
+    finally:
+        K.EVENT_HOOK = None
+    assert "g_a.0.conv1+skip.dgrad" in ran and "g_a.0.skip.dgrad" not in ran, sorted(ran)
     assert rel_err(K.from_nc4(gx4, 3).cpu(), xr.grad) < 2e-3
 
 
