@@ -212,11 +212,12 @@ def _traffic(tfile, dom, table):
     return e["bytes"], f"profiles/{tfile}: {kern}, grid {grid}, src {src}"
 
 
-def cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner, seconds):
+def cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner):
     """configs[3] on the CPU oracle (oracle.attack.adv_train_step: coupled inner attack + train-mode RD step + clip +
-    Adam + aux Adam), bounded: one outer step with 1 inner step and one with 3, on the bench's batch; the inner-step
-    time is their difference / 2, the rest is the train step, and the rate is that of an outer step with `inner`
-    inner steps (the same accounting as the GPU value: inner image-steps per second of whole outer steps)."""
+    Adam + aux Adam).  Not bounded by --cpu-seconds: it always times a warm-up outer step and one outer step each with
+    1 and 3 inner steps, on the bench's batch (≈10-20 s on 16 cores); the inner-step time is their difference / 2, the
+    rest is the train step, and the rate is an EXTRAPOLATION to an outer step with `inner` inner steps (the same
+    accounting as the GPU value: inner image-steps per second of whole outer steps)."""
     from oracle import attack as oa
     from oracle import codec
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0)))))
@@ -334,7 +335,7 @@ def bench_finetune(args):
             "roofline": roof(dom), "wgrad_roofline": roof(wdom),
             "per_kernel_ms_total_per_outer_step": {k: round(v / args.steps, 3) for k, v in sorted(tot_ms.items())},
             "cpu_baseline": (None if world > 1 or args.no_cpu_baseline else
-                             cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner, args.cpu_seconds)),
+                             cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner)),
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -178,7 +178,7 @@ int ica_ar_step(const ica_ar_args* a, int p0, int p1, int mode, hipStream_t st) 
   ArArgs k;
   static_assert(sizeof(ArArgs) == sizeof(ica_ar_args), "ArArgs mirrors ica_ar_args");
   std::memcpy(&k, a, sizeof(k));
-  hipLaunchKernelGGL(ar_step_kernel, dim3(a->B), dim3(256), lds, st, k, p0, p1, mode);
+  ICA_LAUNCH(ar_step_kernel, dim3(a->B), dim3(256), lds, st, k, p0, p1, mode);
   ICA_CHECK_LAUNCH();
   return 0;
 }

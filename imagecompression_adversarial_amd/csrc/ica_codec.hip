@@ -149,7 +149,7 @@ int ica_gc_symbols(const float* y4, const float* scales4, const float* means4, c
                    int32_t* symbols, int32_t* indexes, int B, int C, int H, int W, hipStream_t st) {
   if (T < 1) return -5;
   const long total = (long)B * C * H * W;
-  hipLaunchKernelGGL(gc_symbols_kernel, dim3(grid_1d_codec(total)), dim3(256), 0, st, y4, scales4, means4, table, T,
+  ICA_LAUNCH(gc_symbols_kernel, dim3(grid_1d_codec(total)), dim3(256), 0, st, y4, scales4, means4, table, T,
                      bound, symbols, indexes, total, C, H, W);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -158,7 +158,7 @@ int ica_gc_symbols(const float* y4, const float* scales4, const float* means4, c
 int ica_eb_symbols(const float* z4, const float* medians, int32_t* symbols, int32_t* indexes, int B, int C, int H,
                    int W, hipStream_t st) {
   const long total = (long)B * C * H * W;
-  hipLaunchKernelGGL(eb_symbols_kernel, dim3(grid_1d_codec(total)), dim3(256), 0, st, z4, medians, symbols, indexes,
+  ICA_LAUNCH(eb_symbols_kernel, dim3(grid_1d_codec(total)), dim3(256), 0, st, z4, medians, symbols, indexes,
                      total, C, H, W);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -167,7 +167,7 @@ int ica_eb_symbols(const float* z4, const float* medians, int32_t* symbols, int3
 int ica_dequantize(const int32_t* symbols, const float* means4, const float* medians, float* out4, int B, int C, int H,
                    int W, hipStream_t st) {
   const long total = (long)B * C * H * W;
-  hipLaunchKernelGGL(dequantize_kernel, dim3(grid_1d_codec(total)), dim3(256), 0, st, symbols, means4, medians, out4,
+  ICA_LAUNCH(dequantize_kernel, dim3(grid_1d_codec(total)), dim3(256), 0, st, symbols, means4, medians, out4,
                      total, C, H, W);
   ICA_CHECK_LAUNCH();
   return 0;

@@ -150,14 +150,16 @@ inline int ica_cu_count() {
   return cus;
 }
 
-// The conv launchers record the kernel and grid of their last launch (ICA_LAUNCH), so that a host that just timed
-// a tagged launch can ask which kernel that was (ica_last_launch): bench.py checks its PMC traffic stamps with it.
+// Every launcher records the kernel and grid of its last launch and counts launches (ICA_LAUNCH), so that a host
+// that just timed a tagged launch can ask which kernel that was and whether it was the only one (ica_last_launch
+// consumes the record): bench.py checks its PMC traffic stamps with it.
 struct IcaLaunchRec {
   const void* fn;
   unsigned long long threads;   // grid x block, as rocprofv3's Grid_Size
+  int count;                    // launches since the record was last consumed
 };
 inline IcaLaunchRec& ica_launch_rec() {
-  static thread_local IcaLaunchRec r{nullptr, 0};
+  static thread_local IcaLaunchRec r{nullptr, 0, 0};
   return r;
 }
 template <typename F>
@@ -167,11 +169,48 @@ inline const void* ica_fnptr(F* f) {   // a kernel (function designator or point
 #define ICA_LAUNCH(kern, grid, block, lds, st, ...)                                                           \
   do {                                                                                                       \
     const dim3 ica_g_ = (grid), ica_b_ = (block);                                                                \
-    ica_launch_rec() = IcaLaunchRec{ica_fnptr(kern),                                                        \
-                                    (unsigned long long)ica_g_.x * ica_g_.y * ica_g_.z * ica_b_.x * ica_b_.y * \
-                                        ica_b_.z};                                                           \
+    IcaLaunchRec& ica_r_ = ica_launch_rec();                                                                 \
+    ica_r_ = IcaLaunchRec{ica_fnptr(kern),                                                                   \
+                          (unsigned long long)ica_g_.x * ica_g_.y * ica_g_.z * ica_b_.x * ica_b_.y * ica_b_.z, \
+                          ica_r_.count + 1};                                                                 \
     hipLaunchKernelGGL(kern, ica_g_, ica_b_, lds, st, __VA_ARGS__);                                          \
   } while (0)
+
+// In-kernel clock (diagnostic builds only, -DICA_CLOCK_STAMP via scripts/build_variant.sh; the product library
+// compiles these to nothing).  Wave 0 of each block stamps the shader clock (s_memtime) and the 100 MHz real-time
+// counter at kernel entry (record words 0, 1) and exit (words 6, 7), and optionally the shader clock at phase
+// boundaries (ICA_STAMP_AT(k), words 2..5), into a buffer of its own (ica_diag_stamp_buffer): 8 words per block,
+// slot = linear block id.  clock = d(memtime) / d(memrealtime) * 100 MHz (MI355X_MICROARCH.md, DVFS give-back
+// item 6).  No output element reads or depends on a stamp.
+#ifdef ICA_CLOCK_STAMP
+__device__ unsigned long long* ica_stamp_buf;   // one definition per translation unit built with the flag
+__device__ unsigned ica_stamp_slots;
+ICA_DEV void ica_stamp_put(int w, unsigned long long v) {   // lane 0 of wave 0: one vector store
+  const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (threadIdx.x == 0 && ica_stamp_buf && b < ica_stamp_slots) {
+    unsigned long long vv = v;
+    asm volatile("" : "+v"(vv));
+    ica_stamp_buf[(size_t)b * 8 + w] = vv;
+  }
+}
+#define ICA_STAMP_BEGIN()                                                  \
+  const unsigned long long ica_t0_ = __builtin_amdgcn_s_memtime();         \
+  const unsigned long long ica_r0_ = __builtin_amdgcn_s_memrealtime()
+#define ICA_STAMP_AT(k) ica_stamp_put(2 + (k), __builtin_amdgcn_s_memtime())
+#define ICA_STAMP_END()                                                      \
+  do {                                                                       \
+    const unsigned long long ica_t1_ = __builtin_amdgcn_s_memtime();         \
+    const unsigned long long ica_r1_ = __builtin_amdgcn_s_memrealtime();     \
+    ica_stamp_put(0, ica_t0_);                                               \
+    ica_stamp_put(1, ica_r0_);                                               \
+    ica_stamp_put(6, ica_t1_);                                               \
+    ica_stamp_put(7, ica_r1_);                                               \
+  } while (0)
+#else
+#define ICA_STAMP_BEGIN() ((void)0)
+#define ICA_STAMP_AT(k) ((void)0)
+#define ICA_STAMP_END() ((void)0)
+#endif
 
 #define ICA_CHECK_LAUNCH()                          \
   do {                                              \

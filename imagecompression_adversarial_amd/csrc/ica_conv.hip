@@ -88,14 +88,10 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
   // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
   static_assert(!X6O || (!BF && CC == 16), "x6 conv_down: fp32 fills of 16-channel chunks");
-#ifndef ICA_X6O_SB
   // X6O: [buffer][plane][half][pixel], 8 channels as bf16; the GDN-backward epilogues park g*s in it afterwards
   // (IT*16 floats per lane, one slab per wave)
   constexpr bool XST = X6O && (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) && !(FX == 0 && IT <= 4);
   __shared__ f32x4 patch[X6O ? (XST && IT * 1024 > 12 * PLANE ? IT * 1024 : 12 * PLANE) : NE * PLANE];
-#else
-  __shared__ f32x4 patch[X6O ? 6 * PLANE : NE * PLANE];
-#endif
   // bf16 16-channel-chunk layers: the epilogue parameters in LDS (epi_params_to_lds), copied before the first
   // chunk fill, whose barriers publish them
   // The RGB-input GDN forward too (g_a.0: 1.65 -> 1.31 ms at the config-5 shapes, although its 46 KB of LDS take it
@@ -468,7 +464,6 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
     // run in a 3-set ring two taps ahead (KK = 9 = 3 rings, so a chunk always starts on set 0): a tap's fill load
     // is then younger than the weights consumed for the next three taps, and the in-order vmcnt never waits on it
     // before its own split.  Same MFMA order as the single-buffer loop (bit-identical results).
-#ifndef ICA_X6O_SB
     static_assert(KK % 3 == 0, "x6 conv_down ring: KK a multiple of 3");
     constexpr bool MK = (FX & FX_MASK) != 0, US = (FX & FX_UNSHUF) != 0;
     constexpr int NF = (NE * PLANE + 255) / 256, PUTD = 3;
@@ -556,28 +551,6 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
       }
       __syncthreads();
     }
-#else
-    auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) {
-      const int ch = g / KK, tap = g - ch * KK;
-      if (tap == 0) fill(ch);
-      ldw(nxt, g + 1);
-      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch a step ahead of its use
-      const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-      const int o = h * PLANE + lbase + ky * PC + kx;
-      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
-#pragma unroll
-      for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(cur[it], b, acc[0][it]);
-    };
-    bf16x8 fa[IT][3], fb[IT][3];
-    ldw(fa, 0);
-    int g = 0;
-#pragma unroll 1
-    for (; g + 1 < total; g += 2) {
-      step(fa, fb, g);
-      step(fb, fa, g + 1);
-    }
-    if (g < total) step(fa, fb, g);
-#endif
   } else {
     // Weight fragments stream linearly through (chunk, tap); they are prefetched
     // one tap ahead into the other of two register sets (ping-pong, no copies)
@@ -1978,7 +1951,8 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
 extern "C" {
 int ica_last_launch(char* name, int cap, unsigned long long* threads) {
   const IcaLaunchRec r = ica_launch_rec();
-  if (!r.fn) return -1;
+  ica_launch_rec() = IcaLaunchRec{nullptr, 0, 0};   // consumed: the next query sees only later launches
+  if (!r.fn) return 0;
   if (threads) *threads = r.threads;
   if (name && cap > 0) {
     const char* m = hipKernelNameRefByPtr(r.fn, nullptr);
@@ -1988,7 +1962,7 @@ int ica_last_launch(char* name, int cap, unsigned long long* threads) {
     std::snprintf(name, (size_t)cap, "%s", src);
     std::free(d);
   }
-  return 0;
+  return r.count;
 }
 
 typedef struct ica_conv_args {

@@ -41,6 +41,7 @@ constexpr int xd_th() { return 4 * PT; }
 // --------------------------------------------------------------------------------------------------------------
 template <int IT, int EPI, int PT = X6_PT>
 __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long ps) {
+  ICA_STAMP_BEGIN();
   constexpr int KS = 5, S = 2, PAD = 2, KK = 25, TW = XD_TW, TH = xd_th<PT>();
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;
   constexpr int NF = (4 * PLANE + 255) / 256, NB = (NF + 1) / 2;  // fill items per thread, in two batches
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(256, 1) void conv_down_x6_kernel(ConvParams p, long
       conv_epilogue<IT, EPI, 0, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
     }
   }
+  ICA_STAMP_END();
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -397,6 +399,7 @@ if constexpr (EPI == EPI_BIAS) {
 
 template <int EPI, int PT>
 __global__ __launch_bounds__(512, 1) void conv_down_x6w_kernel(ConvParams p, long ps2) {
+  ICA_STAMP_BEGIN();
   constexpr int IT = 4, ITW = 2, KS = 5, S = 2, PAD = 2, TW = 32, TH = 4 * PT, NS = XW_NS;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS, PLANE = PR * PC;   // 19 x 67
   constexpr int PCE = (PC + 1) / 2;
@@ -550,6 +553,7 @@ __global__ __launch_bounds__(512, 1) void conv_down_x6w_kernel(ConvParams p, lon
     ok[t] = oy[t] < p.Hout && ox < p.Wout;
   }
   xw_epilogue<EPI, PT>(p, acc, n, oy, ox, ok, chh, wave, cb, lds);
+  ICA_STAMP_END();
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -823,8 +827,101 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
   if (u < total) step(fa, fb, ba, bb, u);
 }
 
+#ifdef ICA_MFMA16_AB
+// A/B experiment (timing only; variant builds, scripts/build_variant.sh -DICA_MFMA16_AB): the conv_up_x6 class main
+// loop on v_mfma_f32_16x16x32_bf16.  A K step is 32 deep (a chunk PAIR of one tap); the wave's 128-channel x 64-pixel
+// tile is 8 x 4 blocks of 16 x 16, 6 MFMAs of 16 cycles per block and step: the cycles, operand bytes and register
+// blocking of the 32x32x16 loop (8 row blocks x 3 planes x 1 KB of weights and 4 column blocks x 3 planes of LDS
+// reads per 32 channels).  The weight bytes are the product pack's entries of the two chunks (same addresses, not
+// the 16x16 fragment order) and the accumulators reach the epilogue in the 16x16 block layout: the instruction
+// stream and the traffic are the product's, the values are not.
+ICA_DEV f32x4 mfma16_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+  return c;
+}
+
+template <int PY, int PX, int IT, int CG, int PT, int KS = 5>
+ICA_DEV void conv_up_x6_class16(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch, int grp, long ps,
+                                f32x16 (&acc)[PT][IT]) {
+  constexpr int PAD = KS / 2, XU_PLANE = xu_plane<PT>();
+  constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
+  constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
+  constexpr int NCG = CG / 16, NCP = NCG / 2, RB = 2 * IT, CB = 2 * PT;
+  const int lane = threadIdx.x & 63, q4 = lane >> 4, j16 = lane & 15;
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
+  const int wbase = cb * KS * KS * nch * IT * 64;
+  const int total = NT * NCP;
+  f32x4 a4[RB][CB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int t = c >> 1, it = rb >> 1, k = 2 * (rb & 1) + (c & 1);
+      a4[rb][c] = f32x4{acc[t][it][4 * k], acc[t][it][4 * k + 1], acc[t][it][4 * k + 2], acc[t][it][4 * k + 3]};
+    }
+  auto ldw = [&](bf16x8 (&a)[RB][3], int u) {
+    u = min(u, total - 1);
+    const int ti = u / NCP, cp = u - ti * NCP;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int f = wbase + ((ky * KS + kx) * nch + grp * NCG + 2 * cp) * IT * 64;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        a[rb][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + (rb & 1) * IT * 64 + (rb >> 1) * 64) * 16));
+  };
+  auto ldb = [&](bf16x8 (&b)[CB][3], int u) {
+    u = min(u, total - 1);
+    const int ti = u / NCP, cp = u - ti * NCP;
+    const int ky = KY0 + 2 * (ti / NX), kx = KX0 + 2 * (ti % NX);
+    const int pc = j16 + 1 + (PX + PAD - kx) / 2;
+    const int e = (4 * cp + q4) * XU_PLANE + (jt * 2 * PT + 1 + (PY + PAD - ky) / 2) * XU_PC + pc;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int o = e + c * XU_PC;
+      b[c][0] = f4_as_bf8(patch[o]);
+      b[c][1] = f4_as_bf8(patch[(CG / 8) * XU_PLANE + o]);
+      b[c][2] = f4_as_bf8(patch[2 * (CG / 8) * XU_PLANE + o]);
+    }
+  };
+  auto step = [&](bf16x8 (&cur)[RB][3], bf16x8 (&nxt)[RB][3], bf16x8 (&bc)[CB][3], bf16x8 (&bn)[CB][3], int u) {
+    ldw(nxt, u + 1);
+    ldb(bn, u + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) a4[rb][c] = mfma16_x6(cur[rb], bc[c], a4[rb][c]);
+  };
+  bf16x8 fa[RB][3], fb[RB][3], ba[CB][3], bb[CB][3];
+  ldw(fa, 0);
+  ldb(ba, 0);
+  int u = 0;
+#pragma unroll 1
+  for (; u + 1 < total; u += 2) {
+    step(fa, fb, ba, bb, u);
+    step(fb, fa, bb, ba, u + 1);
+  }
+  if (u < total) step(fa, fb, ba, bb, u);
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int t = c >> 1, it = rb >> 1, k = 2 * (rb & 1) + (c & 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][it][4 * k + i] = a4[rb][c][i];
+    }
+}
+#endif
+
 template <int IT, int EPI, int CG, int PT = X6_PT, int KS = 5, int FX = 0>
 __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long ps) {
+  ICA_STAMP_BEGIN();
   constexpr int NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
   extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
   const int tiles_x = (p.Win + XU_TW - 1) / XU_TW, tiles_y = (p.Hin + XU_TH - 1) / XU_TH;
@@ -887,8 +984,14 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
       for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
     for (int grp = 0; grp < ngrp; ++grp) {
       if (refill) fill(grp);
+#ifdef ICA_MFMA16_AB
+      if constexpr (KS == 5 && PT == 2 && IT == 4)
+        conv_up_x6_class16<PY, PX, IT, CG, PT, KS>(p, patch, jt, cb, nch, grp, ps, acc);
+      else
+#endif
       conv_up_x6_class<PY, PX, IT, CG, PT, KS>(p, patch, jt, cb, nch, grp, ps, acc);
     }
+    ICA_STAMP_AT(tk - 2);
     if constexpr ((EPI == EPI_GDN || EPI == EPI_IGDN) && PT == 2) {
       const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
       const int ox[2] = {2 * (b0 + b_rel) + PX, 2 * (b0 + b_rel) + PX};
@@ -900,6 +1003,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
         conv_epilogue<IT, EPI, FX, false, 1>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
       }
     }
+    ICA_STAMP_AT(tk - 1);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -913,6 +1017,7 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
     run_class(I0{}, I1{}, multi, 2);
     run_class(I1{}, I0{}, multi, 4);
   }
+  ICA_STAMP_END();
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -982,6 +1087,7 @@ ICA_DEV void conv_up_x6w_class(const ConvParams& p, const f32x4* patch, int jt, 
 
 template <int IT, int EPI, int CG>
 __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long ps) {
+  ICA_STAMP_BEGIN();
   constexpr int PT = 2, NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
   extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
   const int tiles_x = (p.Win + XU_TW - 1) / XU_TW, tiles_y = (p.Hin + XU_TH - 1) / XU_TH;
@@ -1067,6 +1173,7 @@ __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long 
     case 2: run_class(I1{}, I1{}, multi); break;
     default: run_class(I1{}, I0{}, multi); break;
   }
+  ICA_STAMP_END();
 }
 
 // --------------------------------------------------------------------------------------------------------------
@@ -1868,5 +1975,14 @@ int ica_conv_up3k3_x6(const float* g1, const float* gs, const void* wp, float* d
   ICA_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef ICA_CLOCK_STAMP
+// diagnostic builds only (scripts/clock_probe.py): where the x6 kernels put their entry / exit stamps
+int ica_diag_stamp_buffer(unsigned long long* buf, unsigned slots) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(ica_stamp_buf), &buf, sizeof(buf)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(ica_stamp_slots), &slots, sizeof(slots)) != hipSuccess) return -1;
+  return 0;
+}
+#endif
 
 }  // extern "C"

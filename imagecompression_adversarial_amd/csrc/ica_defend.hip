@@ -113,13 +113,13 @@ extern "C" {
 
 int ica_flip_rot(const float* x, float* y, long planes, int H, int W, int op, hipStream_t st) {
   if (op < 0 || op > 3) return -5;
-  hipLaunchKernelGGL(flip_rot_kernel, dim3(grid_1d_def(planes * H * W)), dim3(256), 0, st, x, y, planes, H, W, op);
+  ICA_LAUNCH(flip_rot_kernel, dim3(grid_1d_def(planes * H * W)), dim3(256), 0, st, x, y, planes, H, W, op);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_bitdepth(const float* x, float* y, long n, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(bitdepth_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, x, y, n, scale);
+  ICA_LAUNCH(bitdepth_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, x, y, n, scale);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -128,32 +128,32 @@ int ica_resample_axis(const float* x, float* y, long planes, int H, int W, int a
                       const int* xsize, const float* w, int K, hipStream_t st) {
   if (axis != 0 && axis != 1) return -5;
   const long total = planes * (axis == 0 ? (long)out_len * W : (long)H * out_len);
-  hipLaunchKernelGGL(resample_axis_kernel, dim3(grid_1d_def(total)), dim3(256), 0, st, x, y, planes, H, W, axis,
+  ICA_LAUNCH(resample_axis_kernel, dim3(grid_1d_def(total)), dim3(256), 0, st, x, y, planes, H, W, axis,
                      out_len, xmin, xsize, w, K);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_bitdepth_noise(const float* x, const float* u, float* y, long n, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(bitdepth_noise_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, x, u, y, n, scale);
+  ICA_LAUNCH(bitdepth_noise_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, x, u, y, n, scale);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_bitdepth_noise_bwd(const float* g, float* gx, long n, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(bitdepth_noise_bwd_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, g, gx, n, scale);
+  ICA_LAUNCH(bitdepth_noise_bwd_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, g, gx, n, scale);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_add(const float* a, const float* b, float* y, long n, hipStream_t st) {
-  hipLaunchKernelGGL(add_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, a, b, y, n);
+  ICA_LAUNCH(add_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, a, b, y, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_ensemble_grad(const float* o, const float* out_s, float* g, long n, float invN, hipStream_t st) {
-  hipLaunchKernelGGL(ensemble_grad_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, o, out_s, g, n, invN);
+  ICA_LAUNCH(ensemble_grad_kernel, dim3(grid_1d_def(n)), dim3(256), 0, st, o, out_s, g, n, invN);
   ICA_CHECK_LAUNCH();
   return 0;
 }

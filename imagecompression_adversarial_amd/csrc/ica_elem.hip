@@ -594,20 +594,20 @@ int ica_elem_blocks_per_image() { return ELEM_BLOCKS_PER_IMAGE; }
 
 int ica_nchw_to_nc4(const float* src, float* dst, int N, int C, int H, int W, hipStream_t st) {
   const long total = (long)N * ((C + 3) / 4) * H * W;
-  hipLaunchKernelGGL(nchw_to_nc4_kernel, dim3(grid_1d(total)), dim3(256), 0, st, src, dst, N, C, H, W);
+  ICA_LAUNCH(nchw_to_nc4_kernel, dim3(grid_1d(total)), dim3(256), 0, st, src, dst, N, C, H, W);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_nc4_to_nchw(const float* src, float* dst, int N, int C, int H, int W, hipStream_t st) {
   const long total = (long)N * ((C + 3) / 4) * H * W;
-  hipLaunchKernelGGL(nc4_to_nchw_kernel, dim3(grid_1d(total)), dim3(256), 0, st, src, dst, N, C, H, W);
+  ICA_LAUNCH(nc4_to_nchw_kernel, dim3(grid_1d(total)), dim3(256), 0, st, src, dst, N, C, H, W);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_reduce_rows(const float* part, float* out, int B, int nblk, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(B), dim3(256), 0, st, part, out, nblk, scale);
+  ICA_LAUNCH(reduce_rows_kernel, dim3(B), dim3(256), 0, st, part, out, nblk, scale);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -615,7 +615,7 @@ int ica_reduce_rows(const float* part, float* out, int B, int nblk, float scale,
 // part must hold B * ica_elem_blocks_per_image() floats.
 int ica_attack_prologue_ex(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W,
                            float eps, int clamp_in, hipStream_t st) {
-  hipLaunchKernelGGL(attack_prologue_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, im_in4,
+  ICA_LAUNCH(attack_prologue_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, im_in4,
                      part, (long)H * W, eps, clamp_in);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -628,7 +628,7 @@ int ica_attack_prologue(const float* noise, const float* im_s, float* im_in4, fl
 
 int ica_attack_loss(const float* xhat4, const float* out_s, float* grad4, float* part, int B, int H, int W,
                     float invN, int clamp, int mode, hipStream_t st) {
-  hipLaunchKernelGGL(attack_loss_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, xhat4, out_s, grad4, part,
+  ICA_LAUNCH(attack_loss_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, xhat4, out_s, grad4, part,
                      (long)H * W, invN, clamp, mode);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -638,7 +638,7 @@ int ica_attack_adam_ex(float* noise, const float* im_s, const float* gnet4, cons
                        const float* cheap_grad, float* m, float* v, float* im_in_out, int B, int H, int W, float eps,
                        float thr, float invN, float bc2s, float neg_step, int* branch, const int* gpos, int* census,
                        int clamp_in, hipStream_t st) {
-  hipLaunchKernelGGL(attack_adam_kernel<false>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
+  ICA_LAUNCH(attack_adam_kernel<false>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
                      loss_i, cheap_grad, m, v, im_in_out, (long)H * W, eps, thr, invN, bc2s, neg_step, branch,
                      RoiBox{}, (long)W, gpos, census, clamp_in);
   ICA_CHECK_LAUNCH();
@@ -655,7 +655,7 @@ int ica_attack_adam(float* noise, const float* im_s, const float* gnet4, const f
 int ica_roi_prologue(const float* noise, const float* im_s, float* im_in4, float* part, int B, int H, int W, float eps,
                      int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, hipStream_t st) {
   const RoiBox roi{x0, x1, y0, y1, w_in_tar, w_in_bkg, 0.f, 0.f};
-  hipLaunchKernelGGL(roi_prologue_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, im_in4, part,
+  ICA_LAUNCH(roi_prologue_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, im_in4, part,
                      (long)H * W, (long)W, eps, roi);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -664,7 +664,7 @@ int ica_roi_prologue(const float* noise, const float* im_s, float* im_in4, float
 int ica_roi_loss(const float* xhat4, const float* out_s, const float* out_t, float* grad4, float* part, int B, int H,
                  int W, int x0, int x1, int y0, int y1, float w_out_tar, float w_out_bkg, int clamp, hipStream_t st) {
   const RoiBox roi{x0, x1, y0, y1, 0.f, 0.f, w_out_tar, w_out_bkg};
-  hipLaunchKernelGGL(roi_loss_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, xhat4, out_s, out_t, grad4,
+  ICA_LAUNCH(roi_loss_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, xhat4, out_s, out_t, grad4,
                      part, (long)H * W, (long)W, roi, clamp);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -675,7 +675,7 @@ int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const floa
                  int x0, int x1, int y0, int y1, float w_in_tar, float w_in_bkg, const int* gpos, int* census,
                  hipStream_t st) {
   const RoiBox roi{x0, x1, y0, y1, w_in_tar, w_in_bkg, 0.f, 0.f};
-  hipLaunchKernelGGL(attack_adam_kernel<true>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
+  ICA_LAUNCH(attack_adam_kernel<true>, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, noise, im_s, gnet4,
                      loss_i, nullptr, m, v, im_in_out, (long)H * W, eps, thr, 0.f, bc2s, neg_step, branch, roi,
                      (long)W, gpos, census, 1);
   ICA_CHECK_LAUNCH();
@@ -683,7 +683,7 @@ int ica_roi_adam(float* noise, const float* im_s, const float* gnet4, const floa
 }
 
 int ica_branch_select(const float* loss_i, float thr, int B, int* sel, int* gpos, hipStream_t st) {
-  hipLaunchKernelGGL(branch_select_kernel, dim3(1), dim3(64), 0, st, loss_i, thr, B, sel, gpos);
+  ICA_LAUNCH(branch_select_kernel, dim3(1), dim3(64), 0, st, loss_i, thr, B, sel, gpos);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -693,7 +693,7 @@ int ica_gather_images(const float* src, float* dst, const int* idx, int E, long 
   if (floats_per_image % 4) return (int)hipErrorInvalidValue;
   const long quads = floats_per_image / 4;
   const int gx = (int)((quads + 255) / 256 < 1024 ? (quads + 255) / 256 : 1024);
-  hipLaunchKernelGGL(gather_images_kernel, dim3(gx, E), dim3(256), 0, st, reinterpret_cast<const f32x4*>(src),
+  ICA_LAUNCH(gather_images_kernel, dim3(gx, E), dim3(256), 0, st, reinterpret_cast<const f32x4*>(src),
                      reinterpret_cast<f32x4*>(dst), idx, quads);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -701,14 +701,14 @@ int ica_gather_images(const float* src, float* dst, const int* idx, int E, long 
 
 int ica_ifgsm_step(float* x, const float* im_s, const float* grad4, float* gacc, const float* l1, int B, int H,
                    int W, float alpha, float eps, int momentum, hipStream_t st) {
-  hipLaunchKernelGGL(ifgsm_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x, im_s, grad4, gacc, l1,
+  ICA_LAUNCH(ifgsm_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x, im_s, grad4, gacc, l1,
                      (long)H * W, alpha, eps, momentum);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_l1_partial(const float* g4, float* part, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(l1_partial_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, g4, part, (long)H * W);
+  ICA_LAUNCH(l1_partial_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, g4, part, (long)H * W);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -716,7 +716,7 @@ int ica_l1_partial(const float* g4, float* part, int B, int H, int W, hipStream_
 int ica_gc_likelihood(const float* y, const float* scales, const float* means, const float* qnoise, float* y_hat,
                       float* lik, float* part, int B, int C, int H, int W, int training, hipStream_t st) {
   const long per_image = 4L * ((C + 3) / 4) * H * W;
-  hipLaunchKernelGGL(gc_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, y, scales, means, qnoise, y_hat,
+  ICA_LAUNCH(gc_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, y, scales, means, qnoise, y_hat,
                      lik, part, C, per_image, training);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -725,7 +725,7 @@ int ica_gc_likelihood(const float* y, const float* scales, const float* means, c
 int ica_eb_likelihood(const float* z, const float* prm, const float* med, const float* qnoise, float* z_hat,
                       float* lik, float* part, int B, int C, int H, int W, int training, hipStream_t st) {
   const long per_image = 4L * ((C + 3) / 4) * H * W;
-  hipLaunchKernelGGL(eb_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, z, prm, med, qnoise, z_hat, lik,
+  ICA_LAUNCH(eb_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, z, prm, med, qnoise, z_hat, lik,
                      part, C, per_image, training);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -735,14 +735,14 @@ int ica_eb_likelihood(const float* z, const float* prm, const float* med, const 
 // _matrix0.._matrix4, _bias0.._bias4, _factor0.._factor3, then quantiles [C][1][3].
 int ica_pack_eb(const float* const* params, float* prm, float* med, int C, hipStream_t st) {
   const float* const* p = params;
-  hipLaunchKernelGGL(pack_eb_kernel, dim3((C + 63) / 64), dim3(64), 0, st, p[0], p[1], p[2], p[3], p[4], p[5], p[6],
+  ICA_LAUNCH(pack_eb_kernel, dim3((C + 63) / 64), dim3(64), 0, st, p[0], p[1], p[2], p[3], p[4], p[5], p[6],
                      p[7], p[8], p[9], p[10], p[11], p[12], p[13], p[14], prm, med, C);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_round(const float* x, float* y, long n, hipStream_t st) {
-  hipLaunchKernelGGL(round_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
+  ICA_LAUNCH(round_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -750,7 +750,7 @@ int ica_round(const float* x, float* y, long n, hipStream_t st) {
 // n must be a multiple of 4 (nChw4c tensors)
 int ica_cast_f32_bf16(const float* x, void* y, long n, hipStream_t st) {
   if (n % 4) return -2;
-  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_1d(n / 4)), dim3(256), 0, st, reinterpret_cast<const f32x4*>(x),
+  ICA_LAUNCH(cast_f32_bf16_kernel, dim3(grid_1d(n / 4)), dim3(256), 0, st, reinterpret_cast<const f32x4*>(x),
                      reinterpret_cast<u32x2*>(y), n / 4);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -758,40 +758,40 @@ int ica_cast_f32_bf16(const float* x, void* y, long n, hipStream_t st) {
 
 int ica_cast_bf16_f32(const void* x, float* y, long n, hipStream_t st) {
   if (n % 4) return -2;
-  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_1d(n / 4)), dim3(256), 0, st, reinterpret_cast<const u32x2*>(x),
+  ICA_LAUNCH(cast_bf16_f32_kernel, dim3(grid_1d(n / 4)), dim3(256), 0, st, reinterpret_cast<const u32x2*>(x),
                      reinterpret_cast<f32x4*>(y), n / 4);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_abs(const float* x, float* y, long n, hipStream_t st) {
-  hipLaunchKernelGGL(abs_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
+  ICA_LAUNCH(abs_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_nc4_bound_to_nchw(const float* x4, float* out, int B, int H, int W, int clamp, hipStream_t st) {
-  hipLaunchKernelGGL(nc4_bound_to_nchw_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x4, out, (long)H * W,
+  ICA_LAUNCH(nc4_bound_to_nchw_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x4, out, (long)H * W,
                      clamp);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_bound_bwd_nc4(const float* x4, const float* g, float* g4, int B, int H, int W, int clamp, hipStream_t st) {
-  hipLaunchKernelGGL(bound_bwd_nc4_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x4, g, g4, (long)H * W,
+  ICA_LAUNCH(bound_bwd_nc4_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, x4, g, g4, (long)H * W,
                      clamp);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_clamp01(const float* x, float* y, long n, hipStream_t st) {
-  hipLaunchKernelGGL(clamp01_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
+  ICA_LAUNCH(clamp01_kernel, dim3(grid_1d(n)), dim3(256), 0, st, x, y, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_sqdiff_partial(const float* a, const float* b, float* part, int B, long len, int clamp_a, hipStream_t st) {
-  hipLaunchKernelGGL(sqdiff_partial_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, a, b, part, len,
+  ICA_LAUNCH(sqdiff_partial_kernel, dim3(ELEM_BLOCKS_PER_IMAGE, B), dim3(256), 0, st, a, b, part, len,
                      clamp_a);
   ICA_CHECK_LAUNCH();
   return 0;

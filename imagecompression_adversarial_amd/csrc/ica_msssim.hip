@@ -351,11 +351,11 @@ int ica_msssim_level(const float* X, const float* Y, int P, int H, int W, const 
   MsWin m = make_win(win, ws);
   dim3 grid(nblk, P);
   if (mode == 1)
-    hipLaunchKernelGGL(msssim_level_kernel<1>, grid, dim3(256), 0, st, X, Y, H, W, m, C1, C2, part, maps, wgt);
+    ICA_LAUNCH(msssim_level_kernel<1>, grid, dim3(256), 0, st, X, Y, H, W, m, C1, C2, part, maps, wgt);
   else
-    hipLaunchKernelGGL(msssim_level_kernel<0>, grid, dim3(256), 0, st, X, Y, H, W, m, C1, C2, part, maps, wgt);
+    ICA_LAUNCH(msssim_level_kernel<0>, grid, dim3(256), 0, st, X, Y, H, W, m, C1, C2, part, maps, wgt);
   ICA_CHECK_LAUNCH();
-  hipLaunchKernelGGL(msssim_sum_kernel, dim3(P), dim3(256), 0, st, part, out, nblk, 1.0f / ((float)Ho * (float)Wo));
+  ICA_LAUNCH(msssim_sum_kernel, dim3(P), dim3(256), 0, st, part, out, nblk, 1.0f / ((float)Ho * (float)Wo));
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -366,9 +366,9 @@ int ica_msssim_level_bwd(const float* X, const float* Y, const float* maps, int 
   MsWin m = make_win(win, ws);
   dim3 grid(((W + MS_T - 1) / MS_T) * ((H + MS_T - 1) / MS_T), P);
   if (mode == 1)
-    hipLaunchKernelGGL(msssim_bwd_kernel<1>, grid, dim3(256), 0, st, X, Y, maps, H, W, m, gX, gY);
+    ICA_LAUNCH(msssim_bwd_kernel<1>, grid, dim3(256), 0, st, X, Y, maps, H, W, m, gX, gY);
   else
-    hipLaunchKernelGGL(msssim_bwd_kernel<0>, grid, dim3(256), 0, st, X, Y, maps, H, W, m, gX, gY);
+    ICA_LAUNCH(msssim_bwd_kernel<0>, grid, dim3(256), 0, st, X, Y, maps, H, W, m, gX, gY);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -378,7 +378,7 @@ int ica_avgpool2(const float* X, float* Yo, int P, int H, int W, int ph, int pw,
   const long total = (long)P * Ho * Wo;
   long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(avgpool2_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, st, X, Yo, P, H, W, ph, pw);
+  ICA_LAUNCH(avgpool2_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, st, X, Yo, P, H, W, ph, pw);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -387,7 +387,7 @@ int ica_avgpool2_bwd(const float* gO, float* gX, int P, int H, int W, int ph, in
   const long total = (long)P * H * W;
   long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(avgpool2_bwd_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, st, gO, gX, P, H, W, ph, pw);
+  ICA_LAUNCH(avgpool2_bwd_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, st, gO, gX, P, H, W, ph, pw);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -395,7 +395,7 @@ int ica_avgpool2_bwd(const float* gO, float* gX, int P, int H, int W, int ph, in
 int ica_msssim_combine(const float* lvl, int P, int G, int mode, const float* dval, float* val, float* wgt,
                        const float* nout, hipStream_t st) {
   const int groups = (P + G - 1) / G;
-  hipLaunchKernelGGL(msssim_combine_kernel, dim3((groups + 63) / 64), dim3(64), 0, st, lvl, P, G, mode, dval, val, wgt,
+  ICA_LAUNCH(msssim_combine_kernel, dim3((groups + 63) / 64), dim3(64), 0, st, lvl, P, G, mode, dval, val, wgt,
                      nout[0], nout[1], nout[2], nout[3], nout[4]);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -404,7 +404,7 @@ int ica_msssim_combine(const float* lvl, int P, int G, int mode, const float* dv
 int ica_scale(float* x, long n, float s, hipStream_t st) {
   long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(scale_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, st, x, n, s);
+  ICA_LAUNCH(scale_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, st, x, n, s);
   ICA_CHECK_LAUNCH();
   return 0;
 }

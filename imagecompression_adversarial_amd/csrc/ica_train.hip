@@ -392,53 +392,53 @@ int ica_wgrad(const float* Sm, const float* Lg, float* ws, float* out, int N, in
               int Wb, int KS, int S, int P, int nsplit, int accumulate, hipStream_t st) {
   dim3 grid((A + 31) / 32, (Bc + 31) / 32, nsplit);
   if (KS == 5 && S == 2)
-    hipLaunchKernelGGL((wgrad_kernel<5, 2>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
+    ICA_LAUNCH((wgrad_kernel<5, 2>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
   else if (KS == 3 && S == 1)
-    hipLaunchKernelGGL((wgrad_kernel<3, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
+    ICA_LAUNCH((wgrad_kernel<3, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
   else if (KS == 1 && S == 1)
-    hipLaunchKernelGGL((wgrad_kernel<1, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
+    ICA_LAUNCH((wgrad_kernel<1, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
   else
     return -6;
   ICA_CHECK_LAUNCH();
   const long n = (long)A * Bc * KS * KS;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(g1d(n)), dim3(256), 0, st, ws, out, n, nsplit, accumulate);
+  ICA_LAUNCH(split_reduce_kernel, dim3(g1d(n)), dim3(256), 0, st, ws, out, n, nsplit, accumulate);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_channel_sum(const float* x, float* out, int N, int C, int H, int W, int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(C), dim3(256), 0, st, x, out, N, C, (long)H * W, accumulate);
+  ICA_LAUNCH(channel_sum_kernel, dim3(C), dim3(256), 0, st, x, out, N, C, (long)H * W, accumulate);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_relu_bwd(float* g, const float* y, long n, hipStream_t st) {
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, g, y, n);
+  ICA_LAUNCH(relu_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, g, y, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_abs_bwd(float* g, const float* x, long n, hipStream_t st) {
-  hipLaunchKernelGGL(abs_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, g, x, n);
+  ICA_LAUNCH(abs_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, g, x, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_gdn_xsq(const float* y, const float* s, float* out, long n, hipStream_t st) {
-  hipLaunchKernelGGL(gdn_xsq_kernel, dim3(g1d(n)), dim3(256), 0, st, y, s, out, n);
+  ICA_LAUNCH(gdn_xsq_kernel, dim3(g1d(n)), dim3(256), 0, st, y, s, out, n);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_reparam_bwd(const float* p, const float* gprime, float* gout, long n, float bound, int accumulate,
                     hipStream_t st) {
-  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, p, gprime, gout, n, bound, accumulate);
+  ICA_LAUNCH(reparam_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, p, gprime, gout, n, bound, accumulate);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_bpp_grad(const float* lik, float* g, long n, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(bpp_grad_kernel, dim3(g1d(n)), dim3(256), 0, st, lik, g, n, scale);
+  ICA_LAUNCH(bpp_grad_kernel, dim3(g1d(n)), dim3(256), 0, st, lik, g, n, scale);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -446,7 +446,7 @@ int ica_bpp_grad(const float* lik, float* g, long n, float scale, hipStream_t st
 int ica_gc_bwd(const float* yt, const float* sigma, const float* gl, float* gy, float* gs, int B, int C, int H, int W,
                hipStream_t st) {
   const long per_image = 4L * ((C + 3) / 4) * H * W;
-  hipLaunchKernelGGL(gc_bwd_kernel, dim3(g1d(per_image * B)), dim3(256), 0, st, yt, sigma, gl, gy, gs, C, per_image,
+  ICA_LAUNCH(gc_bwd_kernel, dim3(g1d(per_image * B)), dim3(256), 0, st, yt, sigma, gl, gy, gs, C, per_image,
                      B);
   ICA_CHECK_LAUNCH();
   return 0;
@@ -454,7 +454,7 @@ int ica_gc_bwd(const float* yt, const float* sigma, const float* gl, float* gy, 
 
 int ica_eb_bwd(const float* v4, const float* gl4, const float* prm, float* gv4, float* gprm, int N, int C, int H, int W,
                hipStream_t st) {
-  hipLaunchKernelGGL(eb_bwd_kernel, dim3(C), dim3(256), 0, st, v4, gl4, prm, gv4, gprm, N, C, (long)H * W);
+  ICA_LAUNCH(eb_bwd_kernel, dim3(C), dim3(256), 0, st, v4, gl4, prm, gv4, gprm, N, C, (long)H * W);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -466,13 +466,13 @@ int ica_eb_param_scatter(const float* gprm, const float* const* raw, float* cons
     P.raw[i] = raw[i];
     P.grad[i] = graw[i];
   }
-  hipLaunchKernelGGL(eb_param_scatter_kernel, dim3((C + 63) / 64), dim3(64), 0, st, gprm, P, C);
+  ICA_LAUNCH(eb_param_scatter_kernel, dim3((C + 63) / 64), dim3(64), 0, st, gprm, P, C);
   ICA_CHECK_LAUNCH();
   return 0;
 }
 
 int ica_mse_grad(const float* xh4, const float* x, float* g4, int B, int H, int W, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(mse_grad_kernel, dim3(256, B), dim3(256), 0, st, xh4, x, g4, (long)H * W, scale);
+  ICA_LAUNCH(mse_grad_kernel, dim3(256, B), dim3(256), 0, st, xh4, x, g4, (long)H * W, scale);
   ICA_CHECK_LAUNCH();
   return 0;
 }

@@ -282,8 +282,6 @@ class ChengSynthesis:
                 s = torch.empty_like(r) if save else None
                 h = cv.forward(a1, K.EPI_IGDN, gdn=gd, res=r, save_x=yg, save_s=s, tag=f"{t}.conv.fwd")
                 del r
-                if save and i == 0:
-                    a1._ica_in_hw = (x4.shape[2], x4.shape[3])   # the image size, for the fused input gradient
                 saved.append((a1, yg, s) if save else None)
         xh = self.last.forward(h, K.EPI_BIAS, tag=f"{self.tag}.7.fwd")
         return xh, saved

@@ -29,6 +29,8 @@ EVENT_HOOK = None
 def _ev_begin(tag, n):
     if EVENT_HOOK is None or tag is None:
         return None
+    if LAUNCH_HOOK is not None:
+        last_launch()   # consume the launch record: _ev_end sees only this tag's launches
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record()
     return (tag, e0, n)
@@ -66,13 +68,17 @@ def source_hash() -> str:
 
 
 def last_launch():
-    """(demangled kernel name, grid size in threads) of this thread's last conv launch (ica_last_launch): the names
-    and Grid_Size that rocprofv3 reports for the same dispatch."""
+    """(demangled kernel name, grid size in threads) of this thread's only kernel launch since the previous call
+    (ica_last_launch, which consumes the record): the names and Grid_Size that rocprofv3 reports for the same
+    dispatch.  None when there was no launch, ("<N launches>", 0) when there were several (no stamp matches that)."""
     import ctypes as C
     buf = C.create_string_buffer(512)
     thr = C.c_ulonglong(0)
-    if lib().ica_last_launch(buf, 512, C.byref(thr)) != 0:
+    n = lib().ica_last_launch(buf, 512, C.byref(thr))
+    if n <= 0:
         return None
+    if n > 1:
+        return f"<{n} launches>", 0
     return buf.value.decode(errors="replace"), int(thr.value)
 
 

@@ -246,10 +246,12 @@ typedef struct ica_conv_args {
                * another, so a transposed conv's output-parity classes write and read dense lines */
 } ica_conv_args;
 int ica_conv_ex(const ica_conv_args* args, hipStream_t stream);
-/* Evidence, not compute: the kernel and grid of the calling thread's last conv launch (any conv entry point of
- * ica_conv.hip / ica_conv_x6.hip).  name receives the demangled kernel name as rocprofv3 prints it (truncated to
- * cap - 1 chars), *threads the grid size in threads (rocprofv3's Grid_Size).  Returns 0, or -1 before any launch.
- * bench.py matches its PMC traffic stamps (profiles/pmc_traffic*.json) against the launch it timed. */
+/* Evidence, not compute: the kernel and grid of the calling thread's last kernel launch (any entry point of this
+ * library), and how many launches there were since the previous call, which consumes the record.  name receives the
+ * demangled kernel name as rocprofv3 prints it (truncated to cap - 1 chars), *threads the grid size in threads
+ * (rocprofv3's Grid_Size).  Returns the launch count (0: none since the previous call; name and *threads untouched).
+ * bench.py matches its PMC traffic stamps (profiles/pmc_traffic*.json) against the launch it timed, and only when the
+ * timed region held exactly one launch. */
 int ica_last_launch(char* name, int cap, unsigned long long* threads);
 /* Transposed conv to 3 channels (Z-gather kernel): w view [Cin][3][5][5].  layout: 1 = x parity-split
  * (ica_conv_args.layout bit 0; even Hin / Win), 0 = row-major; the 3-channel output is always row-major. */

@@ -1,35 +1,50 @@
-"""Trajectory-sensitivity sweep: cheng2020 q6 attack (2 x 64x64, 4 steps) on the fp32 and x6 HIP paths against the
-oracle over many input seeds; prints the noise deviation (max, fraction beyond 1e-3 of the noise max) per path.
-    python scripts/cheng_seed_sweep.py [n_seeds]     # GPU box
+"""Trajectory sweep: cheng2020 q6 attack (2 x 64x64, 4 steps) on the fp32 and x6 HIP paths over many input seeds, under
+the gate of tests/test_gpu_cheng.py::test_cheng_attack_seeds_vs_float64: the float64 replay of the oracle attack whose
+every network step takes the path's own leaky-ReLU kinks (tests/f64_replay.replay64_path_kinks).  Per seed and path:
+branches kept, every sign disagreement a kink (< KINK_REL of the tensor max), noise elements beyond 1e-3 of the
+float64 noise max, and, for reference, the deviation from the plain fp32 oracle (kinks unmatched).
+    python scripts/cheng_seed_sweep.py [n_seeds] [first_seed]     # GPU box
 """
 import os
 import sys
 
+import pytest
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import attack as oa          # noqa: E402  (checker only)
 from oracle import codec as oc           # noqa: E402
-from imagecompression_adversarial_amd.attack import attack_batch              # noqa: E402
+from tests.f64_replay import KINK_REL, confined, replay64_path_kinks   # noqa: E402
 from imagecompression_adversarial_amd.engine_cheng import ChengKernels        # noqa: E402
 
 DEV = torch.device("cuda:0")
 P = oc.perturb_params(oc.init_params("cheng2020", 6, seed=0), seed=1)
 kern = {pr: ChengKernels({k: v.to(DEV) for k, v in P.items()}, precision=pr) for pr in ("fp32", "x6")}
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-bad = {"fp32": 0, "x6": 0}
-for seed in range(100, 100 + n):
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+first = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+fail = {"fp32": [], "x6": []}
+unmatched = {"fp32": 0, "x6": 0}
+mp = pytest.MonkeyPatch()
+for seed in range(first, first + n):
     g = torch.Generator().manual_seed(seed)
     x = torch.rand((2, 3, 64, 64), generator=g)
-    rec = []
-    ref = oa.attack(P, x, steps=4, noise_thr=1e-5, model="cheng2020", eval_msssim=False, record=rec)
+    ref = oa.attack(P, x, steps=4, noise_thr=1e-5, model="cheng2020", eval_msssim=False)
     line = []
     for pr, k in kern.items():
-        res = attack_batch(k, x.to(DEV), steps=4, noise_thr=1e-5, eval_msssim=False, record=True)
-        same = all([bool(v) for v in br] == [bool(v) for v in rec[i]["cheap"]] for i, br in enumerate(res.branches))
-        d = (res.noise.cpu() - ref.noise).abs() / ref.noise.abs().max()
-        out = float((d > 1e-3).float().mean())
-        bad[pr] += int(out > 0 or not same)
-        line.append(f"{pr} br {same} max {float(d.max()):.2e} >1e-3 {out:.4f}")
+        noise, output_s, branches, r64, gmin, rec, per_step = replay64_path_kinks(
+            P, k, x, 4, mp, DEV, noise_thr=1e-5, model="cheng2020", eval_msssim=False)
+        same = all([bool(v) for v in br] == [bool(v) for v in rec[i]["cheap"]] for i, br in enumerate(branches))
+        n_bad, _, dmax = confined(noise, r64, gmin)
+        worst = max((w for _, wo in per_step.values() for w in wo), default=0.0)
+        kinks = {i: [len(f) for f in fl] for i, (fl, _) in per_step.items()}
+        d32 = float(((noise.cpu() - ref.noise).abs() / ref.noise.abs().max()).max())
+        unmatched[pr] += int(d32 > 1e-3)
+        ok = same and worst < KINK_REL and n_bad == 0 and dmax <= 1e-3
+        if not ok:
+            fail[pr].append(seed)
+        line.append(f"{pr} {'PASS' if ok else 'FAIL'} br {same} kinks {kinks} disagree {worst:.1e} "
+                    f">1e-3 {n_bad} max {dmax:.2e} (fp32 oracle, unmatched: {d32:.2e})")
     print(f"seed {seed}: " + " | ".join(line), flush=True)
-print("seeds with a deviation beyond 1e-3 or a branch change:", bad)
+mp.undo()
+print(f"{n} seeds; failing the float64 gate with per-step kinks: {fail}; beyond 1e-3 of the plain fp32 oracle: "
+      f"{unmatched}")

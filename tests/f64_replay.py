@@ -146,6 +146,93 @@ def input_grad_flipped(P64, x, gout, flips=()):
     return xr.grad
 
 
+def preacts(P64, x64):
+    """Every leaky-ReLU input of cheng_g_s(cheng_g_a(x)) in float64, in call order (the numbering of kinks())."""
+    from oracle import codec as oc
+    seen = []
+    orig = oc.lrelu
+
+    def rec(a):
+        seen.append(a.detach().clone())
+        return orig(a)
+
+    oc.lrelu = rec
+    try:
+        with torch.no_grad():
+            oc.cheng_g_s(P64, oc.cheng_g_a(P64, x64.detach()))
+    finally:
+        oc.lrelu = orig
+    return seen
+
+
+def path_signs(kern, im_in):
+    """The side of zero (value > 0) of every saved leaky-ReLU output of the path's own forward at im_in (fp32 NCHW on
+    the device), per call in kinks() order, on the CPU: the activations that path's network step differentiated."""
+    from imagecompression_adversarial_amd import hip_ops as K
+    y4, sa = kern.g_a(K.to_nc4(im_in.contiguous()), save=True)
+    _, ss = kern.g_s(y4, save=True)
+    out = []
+    for side, i, slot in lrelu_slots(kern):
+        t = (sa if side == "g_a" else ss)[i][slot]
+        out.append((K.from_nc4(t, t.shape[1] * 4) > 0).cpu())
+    return out
+
+
+KINK_REL = 1e-5   # a kink: a float64 pre-activation within this fraction of its tensor's max of zero
+
+
+def step_flips(P64, x64, signs, rel=KINK_REL):
+    """Per image of x64, the kinks [(call, flat element)] where the path's forward (signs: path_signs at the path's
+    own input of this step) sits on the other side of zero than the float64 pre-activation at x64, and the largest
+    |a| / max|a| over ALL of the image's sign disagreements (a disagreement beyond rel is not a kink: a defect, or an
+    input the float64 trajectory does not share)."""
+    acts = preacts(P64, x64)
+    B = x64.shape[0]
+    flips, worst = [[] for _ in range(B)], [0.0] * B
+    for c, (a, s) in enumerate(zip(acts, signs)):
+        assert a.shape == s.shape, (c, a.shape, s.shape)
+        for b in range(B):
+            ab = a[b].flatten()
+            m = float(ab.abs().max())
+            dis = ((ab > 0) != s[b].flatten()).nonzero().flatten()
+            if dis.numel() == 0:
+                continue
+            r = ab[dis].abs() / m
+            worst[b] = max(worst[b], float(r.max()))
+            flips[b] += [(c, int(e)) for e in dis[r < rel].tolist()]
+    return flips, worst
+
+
+def replay64_path_kinks(P, kern, x, steps, monkeypatch, dev, **kw):
+    """The path's attack (AttackLoop, step by step) and the float64 replay of the oracle attack whose every network
+    step takes the path's own kinks at that step: at step i the path's saved leaky-ReLU outputs, from its forward at
+    its own input im_in_i, are compared with the float64 pre-activations at the replay's input, and the float64
+    forward of each image flips the disagreements within KINK_REL of zero (step_flips).  Returns (path noise, path
+    output_s, path branches, float64 result, gmin, the float64 branch record, per network step {i: (flips per image,
+    largest disagreement per image)})."""
+    from imagecompression_adversarial_amd.attack import AttackLoop
+    loop = AttackLoop(kern, x.to(dev), steps=steps, **{k: kw[k] for k in ("noise_thr", "epsilon", "lr") if k in kw})
+    hip, branches = {}, []
+    for i in range(steps):
+        br = loop.step(i, record_im_in=True, census=True)
+        branches.append(br)
+        idx = [b for b, v in enumerate(br) if not v]
+        if idx:
+            hip[i] = (idx, path_signs(kern, loop.im_in[idx]))
+    P64 = {k: v.double() for k, v in P.items()}
+    per_step = {}
+
+    def expensive(im, i):
+        assert i in hip and len(hip[i][0]) == im.shape[0], f"step {i}: the path's network images differ"
+        fl, worst = step_flips(P64, im, hip[i][1])
+        per_step[i] = (fl, worst)
+        return torch.cat([transforms_flipped(P64, im[b:b + 1], fl[b]) for b in range(im.shape[0])])
+
+    rec = []
+    r64, gmin = replay64(P, x, steps, monkeypatch, record=rec, expensive=expensive, **kw)
+    return loop.noise, loop.output_s, branches, r64, gmin, rec, per_step
+
+
 def match_kinks(P64, x64, gout, gx, tol=2e-5, rel=1e-5, max_flips=2):
     """Per image, the kinks (pre-activations within rel of their tensor's max of zero) with which the float64
     input gradient matches gx: greedy, at most max_flips per image, each round taking the candidate that lowers
