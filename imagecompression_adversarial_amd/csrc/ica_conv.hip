@@ -67,9 +67,12 @@ constexpr int down_pt() { return (BF && CC == 16) ? 2 : 1; }
 template <int KS, int IT>
 constexpr int conv_min_blocks() { return (KS == 5 && IT == 6) ? 1 : 2; }
 
-// the bf16 RGB-input GDN forward (g_a's first layer, store-bound) fits 128 VGPRs: 4 waves/SIMD
+// the bf16 RGB-input GDN forward (g_a's first layer, store-bound) fits 128 VGPRs: 4 waves/SIMD (IT = 4; the
+// C = 192 variant runs one wave per SIMD like every IT = 6 k5 kernel)
 template <int KS, int IT, int CC, int EPI, bool BF>
-constexpr int conv_down_waves() { return (BF && CC == 4 && EPI == EPI_GDN) ? 4 : conv_min_blocks<KS, IT>(); }
+constexpr int conv_down_waves() {
+  return (BF && CC == 4 && EPI == EPI_GDN && IT <= 4) ? 4 : conv_min_blocks<KS, IT>();
+}
 
 // X6O: fp32-accurate bf16x6 operands (fp32 activations split into three bf16 planes as the patch is staged, the
 // three-plane weight pack of ica_pack_conv_weight_x6, six MFMAs per 16-deep k step; x6 GDN epilogue GEMMs on the
@@ -743,9 +746,15 @@ constexpr int up_th() { return 4 * up_pt<BF>(); }
 template <bool BF>
 constexpr int up_plane() { return (up_th<BF>() + 2) * UP_PC; }
 
-// bf16: the epilogue parameters (epi_params_to_lds) sit in LDS right after the whole-Cin patch
-template <bool BF>
-ICA_DEV const f32x4* up_lpar(const f32x4* patch, int nch) { return BF ? patch + 2 * nch * up_plane<BF>() : nullptr; }
+// bf16: the epilogue parameters (epi_params_to_lds) sit in LDS right after the whole-Cin patch (IT <= 4; the IT = 6
+// kernels of the C = 192 layers run one wave per SIMD and load them from global memory: their 75 KB of gamma'
+// fragments next to a 320-channel patch would not fit)
+template <int IT, bool BF>
+constexpr bool up_lg() { return BF && IT <= 4; }
+template <int IT, bool BF>
+ICA_DEV const f32x4* up_lpar(const f32x4* patch, int nch) {
+  return up_lg<IT, BF>() ? patch + 2 * nch * up_plane<BF>() : nullptr;
+}
 
 // Generalised over the kernel size: ConvTranspose2d kKS s2 p(KS/2) op1, i.e. the input-gradient
 // of a stride-2 KSxKS conv with pad KS/2 (KS = 5: g_s deconvs / g_a dgrad; KS = 3, 1: the dgrad of
@@ -879,7 +888,8 @@ ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], 
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-    conv_epilogue<IT, EPI, FX, BF, 0, BF, false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32, lp);
+    conv_epilogue<IT, EPI, FX, BF, 0, up_lg<IT, BF>(), false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout,
+                                                          cb * IT * 32, lp);
   }
 }
 
@@ -888,7 +898,7 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
                            int nch, int tk) {
   f32x16 acc[up_pt<BF>()][IT];
   conv_up_acc<KS, PY, PX, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc);
-  conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
+  conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb, up_lpar<IT, BF>(patch, nch));
   (void)tk;
 }
 
@@ -909,8 +919,8 @@ ICA_DEV void conv_up_pair(const ConvParams& p, const f32x4* patch, int n, int a0
     __builtin_amdgcn_sched_barrier(0);
     conv_up_acc<KS, PY1, PX1, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc1);
     __builtin_amdgcn_sched_barrier(0);
-    conv_up_store<PY0, PX0, IT, EPI, FX, BF>(p, acc0, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
-    conv_up_store<PY1, PX1, IT, EPI, FX, BF>(p, acc1, n, a0, b0, jt, cb, up_lpar<BF>(patch, nch));
+    conv_up_store<PY0, PX0, IT, EPI, FX, BF>(p, acc0, n, a0, b0, jt, cb, up_lpar<IT, BF>(patch, nch));
+    conv_up_store<PY1, PX1, IT, EPI, FX, BF>(p, acc1, n, a0, b0, jt, cb, up_lpar<IT, BF>(patch, nch));
   } else {
     conv_up_class<KS, PY0, PX0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch, 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the second class's prologue out of the first epilogue
@@ -941,7 +951,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(
       reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * qbytes, Cin4 * xplane * qbytes);
   constexpr int UP_FB = 8;
-  if constexpr (BF) epi_params_to_lds<IT, EPI>(p, patch + total, cb * IT * 32);   // published by the fill's barrier
+  if constexpr (up_lg<IT, BF>()) epi_params_to_lds<IT, EPI>(p, patch + total, cb * IT * 32);   // published by the fill's barrier
   for (int e0 = threadIdx.x; e0 < total; e0 += 256 * UP_FB) {
     u32x4_t v[UP_FB];
 #pragma unroll
@@ -1745,16 +1755,18 @@ static int pick_tw_down(const ConvParams& p, hipStream_t st) {
   return launch_down<KS, S, IT, CC, 16, EPI, FX, BF>(p, st);
 }
 
-// bf16-operand variants: the bmshj2018 g_a forward / g_s input-gradient layers (k5 s2, 16-channel chunks)
+// bf16-operand variants: the bmshj2018 g_a forward / g_s input-gradient layers (k5 s2, 16-channel chunks); IT = 6:
+// the C = 192 GDN / IGDN-backward layers of q6-8 (one wave per SIMD, the whole register file)
 template <int KS, int S, int IT, int EPI, int FX>
 constexpr bool down_bf() {
-  return KS == 5 && S == 2 && FX == 0 && (IT == 3 || IT == 4) &&
-         (EPI == EPI_BIAS || EPI == EPI_GDN || EPI == EPI_IGDN_BWD);
+  return KS == 5 && S == 2 && FX == 0 &&
+         (((IT == 3 || IT == 4) && (EPI == EPI_BIAS || EPI == EPI_GDN || EPI == EPI_IGDN_BWD)) ||
+          (IT == 6 && (EPI == EPI_GDN || EPI == EPI_IGDN_BWD)));
 }
 // ... and the RGB-input ones (g_a.0 forward, g_s.6 input-gradient): 4-channel tap groups
 template <int KS, int S, int IT, int EPI, int FX>
 constexpr bool down_bf4() {
-  return KS == 5 && S == 2 && FX == 0 && IT == 4 && (EPI == EPI_GDN || EPI == EPI_IGDN_BWD);
+  return KS == 5 && S == 2 && FX == 0 && (IT == 4 || IT == 6) && (EPI == EPI_GDN || EPI == EPI_IGDN_BWD);
 }
 
 template <int KS, int S, int IT, int EPI, int FX>
@@ -1859,8 +1871,8 @@ static int launch_up(const ConvParams& p, hipStream_t st) {
   constexpr int UP_TH = up_th<BF>();
   const int tiles = ((p.Win + UP_TW - 1) / UP_TW) * ((p.Hin + UP_TH - 1) / UP_TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  const size_t lds = ((size_t)(p.Cin / (BF ? 8 : 4)) * up_plane<BF>() + (BF ? epi_lds_entries<IT, EPI>() : 0)) *
-                     sizeof(f32x4);
+  const size_t lds = ((size_t)(p.Cin / (BF ? 8 : 4)) * up_plane<BF>() +
+                      (up_lg<IT, BF>() ? epi_lds_entries<IT, EPI>() : 0)) * sizeof(f32x4);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1875,7 +1887,14 @@ static int launch_up(const ConvParams& p, hipStream_t st) {
 
 static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStream_t st) {
   if (p.prec == 1) {  // bf16 operands: the bmshj2018 g_s forward / g_a input-gradient layers
-    if (KS != 5 || fx != 0 || it != 4) return -4;
+    if (KS != 5 || fx != 0 || (it != 4 && it != 6)) return -4;
+    if (it == 6) {   // C = 192 (q6-8): the IGDN forward and GDN input-gradient layers
+      switch (epi) {
+        case EPI_IGDN: return launch_up<5, 6, EPI_IGDN, 0, true>(p, st);
+        case EPI_GDN_BWD: return launch_up<5, 6, EPI_GDN_BWD, 0, true>(p, st);
+        default: return -5;
+      }
+    }
     switch (epi) {
       case EPI_BIAS: return launch_up<5, 4, EPI_BIAS, 0, true>(p, st);
       case EPI_IGDN: return launch_up<5, 4, EPI_IGDN, 0, true>(p, st);

@@ -439,12 +439,12 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
     // never live in two versions across a branch (that doubled the register footprint).
     const Img Y(p.y, img, n), IX(p.in_x, img, n), IS(p.in_s, img, n);
     if constexpr (BF) {
-      // bf16 path (FX == 0, IT <= 4): ONE pass over the saved (y, s) — the second read of them was the
-      // epilogue's latency cost at 2 waves/SIMD.  Per element: t (-> a bf16 B fragment), g*s in place of g,
+      // bf16 path (FX == 0): ONE pass over the saved (y, s) — the second read of them was the epilogue's latency
+      // cost at 2 waves/SIMD (IT = 6, the C = 192 layers: one wave per SIMD, the whole register file).  Per element: t (-> a bf16 B fragment), g*s in place of g,
       // and 2x = 2 y rcp(s) kept as bf16 (the saved y and s are bf16 already); then per output tile
       // u = gamma'^T t (bf16 MFMAs, gamma' hi part) and dx = g s + 2x u, stores only.  t, gamma' and 2x rounded
       // to bf16 add 2^-9-relative errors, the size of the bf16 storage of y and s.
-      static_assert(!BF || (FX == 0 && IT <= 4), "bf16 GDN-bwd epilogue: plain, IT <= 4");
+      static_assert(!BF || FX == 0, "bf16 GDN-bwd epilogue: plain layers");
       bf16x8 th[IT][2];
       u32x2 x2q[IT][4];
       // unconditional loads (one basic block, all in flight): a pixel outside the output reads past the

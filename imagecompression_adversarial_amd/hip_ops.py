@@ -259,10 +259,9 @@ class PackedConv:
         """prec=PREC_BF16 packs the k5 s2 layers as bf16 fragments (fwd_prec / bwd_prec record what each pack
         is): 16-channel chunks, 4-tap groups for an RGB conv input, the Z-gather pack for 3-channel outputs.
         it_fwd / it_bwd: 32-channel row tiles per wave of the forward / input-gradient launches (0 = the library
-        default; 6 for the C = 192 GDN layers of bmshj2018 q6-8, whose epilogue needs all channels in one wave)."""
+        default; 6 for the C = 192 GDN layers of bmshj2018 q6-8, whose epilogue needs all channels in one wave; the
+        bf16 path has IT = 6 kernels for those GDN / IGDN layers and their input gradients too)."""
         self.it_fwd, self.it_bwd = it_fwd, it_bwd
-        if prec == PREC_BF16 and (it_fwd or it_bwd):
-            raise NotImplementedError("the bf16 conv path covers the N = 128 transforms (q1-5)")
         if prec == PREC_X6:
             self._init_x6(weight, bias, kind, stride)
             return
@@ -275,7 +274,7 @@ class PackedConv:
             self.Cout, self.Cin = weight.shape[0], weight.shape[1]
             # forward: o = co, c = ci
             if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cin >= 16 or self.Cin <= 4):
-                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN)
+                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN, it=it_fwd)
                 self.fwd_prec = PREC_BF16
             else:
                 self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
@@ -290,7 +289,7 @@ class PackedConv:
                     self.bwd = pack_up3(weight, prec)
                     self.bwd_prec = prec
                 elif prec == PREC_BF16:
-                    self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP)
+                    self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, KK, self.Cin * KK, ORDER_UP, it=it_bwd)
                     self.bwd_prec = PREC_BF16
                 else:
                     self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, ORDER_UP, 16,
@@ -302,14 +301,14 @@ class PackedConv:
                 self.fwd = pack_up3(weight, prec)
                 self.fwd_prec = prec
             elif prec == PREC_BF16 and self.KS == 5:
-                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP)
+                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP, it=it_fwd)
                 self.fwd_prec = PREC_BF16
             else:
                 self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, KK, self.Cout * KK, ORDER_UP, 16,
                                      it=it_fwd)
             # dgrad (conv_down, stride 2): o = ci, c = co
             if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cout >= 16 or self.Cout <= 4):
-                self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN)
+                self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, it=it_bwd)
                 self.bwd_prec = PREC_BF16
             else:
                 self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,

@@ -75,11 +75,13 @@ def main_parameters(net):
     return [p for n, p in net.named_parameters() if not n.endswith(".quantiles")]
 
 
-def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, group=None, world=1, qnoise=None):
+def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, group=None, world=1, qnoise=None,
+             record=None):
     """One outer step of train.py:335-366 on this rank's shard.  The loss of the reference is a mean over the
     GLOBAL batch, so each rank's gradient and loss values (means over its shard) are weighted by
     B_local / B_global and summed over ranks: exact for uneven shards too (one flat all-reduce).
-    qnoise: optional (noise_y, noise_z) train-mode quantisation noise for this shard (tests)."""
+    qnoise: optional (noise_y, noise_z) train-mode quantisation noise for this shard (tests); record: an optional list
+    that receives the inner attack's per-step branch census (one list of per-image cheap flags per step)."""
     batch_x = batch_x.detach().contiguous()
     B_local = batch_x.shape[0]
     if B_local == 0:
@@ -91,7 +93,9 @@ def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, g
     kern = net.kernels(net.attack_precision(getattr(args, "precision", None)))
     res = attack_batch(kern, batch_x, steps=args.steps, epsilon=args.epsilon, noise_thr=args.noise,
                        lr=args.lr_attack, att_metric=args.att_metric, clamp=args.clamp, eval_msssim=False,
-                       coupled=True, group=group)
+                       coupled=True, group=group, record=record is not None)
+    if record is not None:
+        record.extend(res.branches)
     for p in net.parameters():
         p.requires_grad_(True)
     batch_adv = res.im_adv.detach()

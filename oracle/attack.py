@@ -284,15 +284,16 @@ def rd_loss(out, target, metric="mse", lmbda=0.0067):
 
 def adv_train_step(P, batch_x, steps=300, noise_thr=1e-4, epsilon=16.0, lr_attack=0.01, att_metric="L2",
                    clamp=True, model="hyper", metric="mse", lmbda=0.0130, lr_train=1e-4, noise_y=None,
-                   noise_z=None):
+                   noise_z=None, record=None):
     """One outer step of train.py --adv (train.py:335-366): the batch-coupled inner attack (attack_rd.attack_
     on the whole batch, train.py:342), the train-mode forward of the adversarial batch with the given
     quantisation noise, RateDistortionLoss against that same batch (:349-351), backward,
     clip_grad_norm_(1.0) over the main parameters (:360), Adam(lr_train) (:361), then the aux loss of the
     EntropyBottleneck quantiles and its Adam(1e-3) (:363-366; coder.py:50-86 optimiser split).
-    Returns (updated params dict, loss values, aux loss, the adversarial batch)."""
+    Returns (updated params dict, loss values, aux loss, the adversarial batch); record: the inner attack's per-step
+    records (attack())."""
     r = attack(P, batch_x, steps=steps, epsilon=epsilon, noise_thr=noise_thr, lr=lr_attack, att_metric=att_metric,
-               clamp=clamp, model=model, coupled=True, eval_msssim=False)
+               clamp=clamp, model=model, coupled=True, eval_msssim=False, record=record)
     batch_adv = r.im_adv.detach()
     main_names = sorted(k for k in P if not k.endswith(".quantiles"))
     aux_names = sorted(k for k in P if k.endswith(".quantiles"))

@@ -1,8 +1,9 @@
 """Trajectory sweep: cheng2020 q6 attack (2 x 64x64, 4 steps) on the fp32 and x6 HIP paths over many input seeds, under
 the gate of tests/test_gpu_cheng.py::test_cheng_attack_seeds_vs_float64: the float64 replay of the oracle attack whose
 every network step takes the path's own leaky-ReLU kinks (tests/f64_replay.replay64_path_kinks).  Per seed and path:
-branches kept, every sign disagreement a kink (< KINK_REL of the tensor max), noise elements beyond 1e-3 of the
-float64 noise max, and, for reference, the deviation from the plain fp32 oracle (kinks unmatched).
+branches kept, every sign disagreement a kink (< KINK_REL of the tensor max), every noise element beyond 1e-3 of the
+float64 noise max an ill-conditioned one (float64 |g| < 1e-4 max|g| at some step) and none beyond 1e-2, and, for
+reference, the deviation from the plain fp32 oracle (kinks unmatched).
     python scripts/cheng_seed_sweep.py [n_seeds] [first_seed]     # GPU box
 """
 import os
@@ -34,16 +35,16 @@ for seed in range(first, first + n):
         noise, output_s, branches, r64, gmin, rec, per_step = replay64_path_kinks(
             P, k, x, 4, mp, DEV, noise_thr=1e-5, model="cheng2020", eval_msssim=False)
         same = all([bool(v) for v in br] == [bool(v) for v in rec[i]["cheap"]] for i, br in enumerate(branches))
-        n_bad, _, dmax = confined(noise, r64, gmin)
+        n_bad, n_bad_well, dmax = confined(noise, r64, gmin)
         worst = max((w for _, wo in per_step.values() for w in wo), default=0.0)
         kinks = {i: [len(f) for f in fl] for i, (fl, _) in per_step.items()}
         d32 = float(((noise.cpu() - ref.noise).abs() / ref.noise.abs().max()).max())
         unmatched[pr] += int(d32 > 1e-3)
-        ok = same and worst < KINK_REL and n_bad == 0 and dmax <= 1e-3
+        ok = same and worst < KINK_REL and n_bad_well == 0 and dmax <= 1e-2
         if not ok:
             fail[pr].append(seed)
         line.append(f"{pr} {'PASS' if ok else 'FAIL'} br {same} kinks {kinks} disagree {worst:.1e} "
-                    f">1e-3 {n_bad} max {dmax:.2e} (fp32 oracle, unmatched: {d32:.2e})")
+                    f">1e-3 {n_bad} (ill-conditioned {n_bad - n_bad_well}) max {dmax:.2e} (fp32 oracle, unmatched: {d32:.2e})")
     print(f"seed {seed}: " + " | ".join(line), flush=True)
 mp.undo()
 print(f"{n} seeds; failing the float64 gate with per-step kinks: {fail}; beyond 1e-3 of the plain fp32 oracle: "

@@ -46,8 +46,8 @@ cases = {
     "down.igdn_bwd (conv_down_x6w)": (lambda: K.conv_down(x_hi, N, wd.bwd, None, N, 5, 2, K.EPI_IGDN_BWD, gd,
                                                           saved=(sx_lo, ss_lo), prec=wd.bwd_prec), flop + gflop // 4),
     "up.bias (conv_up_x6w)": (lambda: K.conv_up(x_lo, N, wd.fwd, wd.bias, N, K.EPI_BIAS, prec=wd.fwd_prec), flop),
-    "up.gdn_bwd (conv_up_x6, 4 waves)": (lambda: K.conv_up(x_lo, N, wc.bwd, None, N, K.EPI_GDN_BWD, gd,
-                                                           saved=(sx_hi, ss_hi), prec=wc.bwd_prec), flop + gflop),
+    "up.gdn_bwd": (lambda: K.conv_up(x_lo, N, wc.bwd, None, N, K.EPI_GDN_BWD, gd, saved=(sx_hi, ss_hi),
+                                     prec=wc.bwd_prec), flop + gflop),
 }
 cases = {k: v for k, v in cases.items() if only in k}
 L = lib()
@@ -91,6 +91,11 @@ for name, (f, fl) in cases.items():
     if bool((ph > 0).all()):
         marks = torch.cat([st[:, :1], ph, st[:, 6:7]], 1).double()
         d = (marks[:, 1:] - marks[:, :-1]).median(0).values.tolist()
-        print("    wave-0 phases (median cycles): " + ", ".join(
-            f"{k} {v:.0f}" for k, v in zip(("fill+main A", "epilogue A", "main B", "epilogue B", "tail"), d)),
-              flush=True)
+        # conv_up_x6 (4 waves): class A main / epilogue, class B main / epilogue; conv_up_x6w GDN backward: main
+        # loop, block barrier, epilogue of pixel tile 0, of pixel tile 1
+        lab = (("fill+main A", "epilogue A", "main B", "epilogue B", "tail") if "4w" in name else
+               ("fill+main", "barrier", "epilogue t0", "epilogue t1", "tail"))
+        mean = (marks[:, 1:] - marks[:, :-1]).mean(0).tolist()
+        print("    wave-0 phases (median / mean cycles): " + ", ".join(
+            f"{k} {v:.0f} / {m:.0f}" for k, v, m in zip(lab, d, mean)), flush=True)
+    print(f"    block cycles mean {float(dt.mean()):.0f}, p90 {float(dt.quantile(0.9)):.0f}", flush=True)

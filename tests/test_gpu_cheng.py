@@ -459,8 +459,12 @@ def test_cheng_attack_seeds_vs_float64(cheng6, cheng6x6, seed, path, monkeypatch
     pre-activations at the replay's input).  Gates: every sign disagreement between the path and float64 at every
     network step is a kink (within KINK_REL = 1e-5 of its tensor's max of zero: nothing a fp32-accurate forward gets
     wrong away from zero), every branch kept, the output at the fp32 tolerance, and every noise element within 1e-3 of
-    the float64 noise max.  (Round 4 matched kinks at step 0 only; seed 38 then crossed a step-3 kink the replay did not
-    take, and its gate fell back to comparing x6 with the fp32 HIP path.)"""
+    the float64 noise max -- except elements the float64 trajectory itself does not determine at fp32 resolution: those
+    whose float64 gradient falls below ILL = 1e-4 of the step's max|g| at some step, where Adam's g / (|g| + 1e-8)
+    turns an fp32-level gradient error into an O(lr) step (measured: x6 seed 38, one such element at 1.7e-3),
+    bounded at 1e-2.  (Round 4 matched kinks at step 0 only; seed 38 then crossed a step-3 kink the
+    replay did not take -- fp32 23 elements beyond, max 2.3e-2 -- and its gate fell back to comparing x6 with the fp32
+    HIP path.)"""
     from tests.f64_replay import KINK_REL, confined, replay64_path_kinks
     P, kern = cheng6 if path == "fp32" else cheng6x6
     x = rnd((2, 3, 64, 64), seed, 0.0, 1.0)
@@ -472,6 +476,9 @@ def test_cheng_attack_seeds_vs_float64(cheng6, cheng6x6, seed, path, monkeypatch
     steps = {i: ([len(f) for f in fl], [f"{w:.1e}" for w in wo]) for i, (fl, wo) in per_step.items()}
     print(f"{path} seed {seed}: kinks taken per network step (per image count, largest disagreement) {steps}; "
           f"{n_bad} elements beyond 1e-3 of the float64 noise ({n_bad_well} well-conditioned), max {dmax:.3e}")
+    d = (noise.double().cpu() - r64.noise).abs() / r64.noise.abs().max()
+    for e in (d > 1e-3).flatten().nonzero().flatten().tolist():
+        print(f"  element {e}: deviation {float(d.flatten()[e]):.2e}, float64 min |g| / max|g| {float(gmin.flatten()[e]):.1e}")
     assert all(w < KINK_REL for _, wo in per_step.values() for w in wo), per_step
     assert rel_err(output_s.cpu(), r64.output_s.float()) < 2e-4
-    assert n_bad == 0 and dmax <= 1e-3, (n_bad, dmax)
+    assert n_bad_well == 0 and dmax <= 1e-2, (n_bad, n_bad_well, dmax)
