@@ -179,24 +179,27 @@ inline const void* ica_fnptr(F* f) {   // a kernel (function designator or point
 // In-kernel clock (diagnostic builds only, -DICA_CLOCK_STAMP via scripts/build_variant.sh; the product library
 // compiles these to nothing).  Wave 0 of each block stamps the shader clock (s_memtime) and the 100 MHz real-time
 // counter at kernel entry (record words 0, 1) and exit (words 6, 7), and optionally the shader clock at phase
-// boundaries (ICA_STAMP_AT(k), words 2..5), into a buffer of its own (ica_diag_stamp_buffer): 8 words per block,
+// boundaries (ICA_STAMP_AT(k), words 2..5) and per wave (ICA_STAMP_WAVE, words 8..15), into a buffer of its own
+// (ica_diag_stamp_buffer): 16 words per block,
 // slot = linear block id.  clock = d(memtime) / d(memrealtime) * 100 MHz (MI355X_MICROARCH.md, DVFS give-back
 // item 6).  No output element reads or depends on a stamp.
 #ifdef ICA_CLOCK_STAMP
 __device__ unsigned long long* ica_stamp_buf;   // one definition per translation unit built with the flag
 __device__ unsigned ica_stamp_slots;
-ICA_DEV void ica_stamp_put(int w, unsigned long long v) {   // lane 0 of wave 0: one vector store
+ICA_DEV void ica_stamp_put(int w, unsigned long long v, bool any_wave = false) {   // lane 0: one vector store
   const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  if (threadIdx.x == 0 && ica_stamp_buf && b < ica_stamp_slots) {
+  if ((any_wave ? (threadIdx.x & 63) : threadIdx.x) == 0 && ica_stamp_buf && b < ica_stamp_slots) {
     unsigned long long vv = v;
     asm volatile("" : "+v"(vv));
-    ica_stamp_buf[(size_t)b * 8 + w] = vv;
+    ica_stamp_buf[(size_t)b * 16 + w] = vv;
   }
 }
 #define ICA_STAMP_BEGIN()                                                  \
   const unsigned long long ica_t0_ = __builtin_amdgcn_s_memtime();         \
   const unsigned long long ica_r0_ = __builtin_amdgcn_s_memrealtime()
 #define ICA_STAMP_AT(k) ica_stamp_put(2 + (k), __builtin_amdgcn_s_memtime())
+// every wave (up to 8) stamps word 8 + wave: e.g. where each wave's main loop ends
+#define ICA_STAMP_WAVE() ica_stamp_put(8 + (int)(threadIdx.x >> 6), __builtin_amdgcn_s_memtime(), true)
 #define ICA_STAMP_END()                                                      \
   do {                                                                       \
     const unsigned long long ica_t1_ = __builtin_amdgcn_s_memtime();         \
@@ -209,6 +212,7 @@ ICA_DEV void ica_stamp_put(int w, unsigned long long v) {   // lane 0 of wave 0:
 #else
 #define ICA_STAMP_BEGIN() ((void)0)
 #define ICA_STAMP_AT(k) ((void)0)
+#define ICA_STAMP_WAVE() ((void)0)
 #define ICA_STAMP_END() ((void)0)
 #endif
 

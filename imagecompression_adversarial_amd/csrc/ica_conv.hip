@@ -898,7 +898,9 @@ ICA_DEV void conv_up_class(const ConvParams& p, const f32x4* patch, int n, int a
                            int nch, int tk) {
   f32x16 acc[up_pt<BF>()][IT];
   conv_up_acc<KS, PY, PX, IT, EPI, FX, BF>(p, patch, jt, cb, nch, acc);
+  ICA_STAMP_AT(tk - 2);
   conv_up_store<PY, PX, IT, EPI, FX, BF>(p, acc, n, a0, b0, jt, cb, up_lpar<IT, BF>(patch, nch));
+  ICA_STAMP_AT(tk - 1);
   (void)tk;
 }
 
@@ -930,6 +932,7 @@ ICA_DEV void conv_up_pair(const ConvParams& p, const f32x4* patch, int n, int a0
 
 template <int KS, int IT, int EPI, int FX, bool BF>
 __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kernel(ConvParams p) {
+  ICA_STAMP_BEGIN();
   extern __shared__ f32x4 patch[];  // fp32: [Cin/4][TH+2][UP_PC] f32x4; bf16: [Cin/8][TH+2][UP_PC] bf16x8
   constexpr int UP_TH = up_th<BF>(), UP_PLANE = up_plane<BF>();
   const int Hh = p.Hin, Wh = p.Win;
@@ -985,6 +988,7 @@ __global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kern
   } else {
     conv_up_pair<KS, 0, 1, 1, 0, IT, EPI, FX, BF>(p, patch, n, a0, b0, jt, cb, nch);
   }
+  ICA_STAMP_END();
 }
 
 // --------------------------------------------------------------------------
@@ -1968,6 +1972,15 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
 
 // C-ABI argument block of ica_conv_ex (mirrors include/ica_hip.h)
 extern "C" {
+#ifdef ICA_CLOCK_STAMP
+// diagnostic builds only (scripts/clock_probe.py --bf16): where the stamped kernels of this file put their stamps
+int ica_diag_stamp_buffer(unsigned long long* buf, unsigned slots) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(ica_stamp_buf), &buf, sizeof(buf)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(ica_stamp_slots), &slots, sizeof(slots)) != hipSuccess) return -1;
+  return 0;
+}
+#endif
+
 int ica_last_launch(char* name, int cap, unsigned long long* threads) {
   const IcaLaunchRec r = ica_launch_rec();
   ica_launch_rec() = IcaLaunchRec{nullptr, 0, 0};   // consumed: the next query sees only later launches

@@ -748,105 +748,6 @@ __global__ __launch_bounds__(256, 1) void conv_rgb_bwd_x6_kernel(ConvParams p, l
   }
 }
 
-// The RGB-end convs on EIGHT waves, two per SIMD (the conv_down_x6w structure): waves w and w + 4 share a SIMD and
-// split the 128 output channels (64 each) of the same PT 32-pixel rows, so each wave's main loop is 9 steps x 2 tiles
-// x 6 MFMAs per row and its GDN epilogue is xw_epilogue's (the partner's channels of x or t through the LDS exchange
-// area, the GDN GEMM over all 128 channels with the single-wave epilogues' arithmetic).  Block = 4 PT rows x 32
-// output pixels; the 3-plane patch (4 sub-pixel quads) is dead once the main loop ends and the LDS becomes the
-// exchange area.
-template <int EPI, int PT>
-constexpr int rgbw_lds_entries() {
-  constexpr int PLANE = (4 * PT + 2) * 34, XCH = 8 * PT * 2 * 4 * 64;
-  return 3 * 2 * PLANE > XCH ? 3 * 2 * PLANE : XCH;
-}
-template <int EPI, int PT>
-__global__ __launch_bounds__(512, 1) void conv_rgb_x6w_kernel(ConvParams p, long ps) {
-  constexpr int IT = 4, ITW = 2, KK = 9, TW = 32, TH = 4 * PT, PR = TH + 2, PC = TW + 2, PLANE = PR * PC;
-  constexpr int NF = (4 * PLANE + 511) / 512;
-  __shared__ f32x4 lds[rgbw_lds_entries<EPI, PT>()];   // patch [plane][half][pixel], then the exchange area
-  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
-  int bid, cb;
-  xcd_block<true>(bid, cb);
-  const int tx = bid % tiles_x;
-  bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int n = bid / tiles_y;
-  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int rp = wave & 3, chh = wave >> 2;
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const __amdgpu_buffer_rsrc_t xr =
-      uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * p.Hin * p.Win * 16, (unsigned)p.Hin * p.Win * 16u);
-  f32x4 v[NF];
-#pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    const int e = threadIdx.x + 512 * i;
-    const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
-    const int iy = 2 * (oy0 - 1 + pr) + (q >> 1), ix = 2 * (ox0 - 1 + pc) + (q & 1);
-    const bool ok = e < 4 * PLANE && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const unsigned vo = ((unsigned)iy * p.Win + ix) * 16u;
-    v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
-  }
-  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
-  const int wbase = cb * KK * IT * 64 + chh * ITW * 64;
-  auto ldw = [&](bf16x8 (&a)[ITW][3], int g) {
-    const int f = wbase + g * IT * 64;
-#pragma unroll
-    for (int it = 0; it < ITW; ++it)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
-  };
-  bf16x8 fa[ITW][3], fb[ITW][3];
-  ldw(fa, 0);
-  u32x2* p2 = reinterpret_cast<u32x2*>(lds);
-#pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    const int e = threadIdx.x + 512 * i;
-    if (e < 4 * PLANE) {
-      const int q = e / PLANE, pix = e - q * PLANE;
-      u32x2 a, b, c;
-      split3(v[i], a, b, c);
-      const int ent = (q >> 1) * PLANE + pix;
-      p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
-      p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
-      p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
-    }
-  }
-  __syncthreads();
-  f32x16 acc[PT][ITW];
-#pragma unroll
-  for (int t = 0; t < PT; ++t)
-#pragma unroll
-    for (int it = 0; it < ITW; ++it) acc[t][it] = f32x16{0};
-  auto step = [&](bf16x8 (&cur)[ITW][3], bf16x8 (&nxt)[ITW][3], int g) __attribute__((always_inline)) {
-    if (g + 1 < KK) ldw(nxt, g + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    const int ky = g / 3, kx = g - 3 * (g / 3);
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int o = h * PLANE + (PT * rp + t + ky) * PC + j + kx;
-      const bf16x8 b[3] = {f4_as_bf8(lds[o]), f4_as_bf8(lds[2 * PLANE + o]), f4_as_bf8(lds[4 * PLANE + o])};
-#pragma unroll
-      for (int it = 0; it < ITW; ++it) acc[t][it] = mfma_x6(cur[it], b, acc[t][it]);
-    }
-  };
-#pragma unroll
-  for (int g = 0; g < KK; ++g) {
-    if (g & 1) step(fb, fa, g);
-    else step(fa, fb, g);
-  }
-  __syncthreads();   // every wave is done with the patch: the LDS becomes xw_epilogue's exchange area
-  int oy[PT];
-  bool ok[PT];
-  const int ox = ox0 + j;
-#pragma unroll
-  for (int t = 0; t < PT; ++t) {
-    oy[t] = oy0 + PT * rp + t;
-    ok[t] = oy[t] < p.Hout && ox < p.Wout;
-  }
-  xw_epilogue<EPI, PT>(p, acc, n, oy, ox, ok, chh, wave, cb, lds);
-}
-
 // --------------------------------------------------------------------------------------------------------------
 // conv_up_x6: weights [plane][cb][tap][chunk][it][lane] bf16x8.  Output y = 2a + PY uses taps ky = ky0 + 2i,
 // ky0 = (PY + 2) & 1, at input row a + (PY + 2 - ky) / 2 (conv_up_kernel's decomposition).
@@ -1130,10 +1031,10 @@ __global__ __launch_bounds__(256, 1) void conv_up_x6_kernel(ConvParams p, long p
 // conv_up_x6: same bits (scripts/gpu_ab_bits.sh).  Forward layers only (launch_up_x6): bias 2.98 -> 2.73 ms, IGDN
 // 3.66 -> 3.44 ms at the config-2 shapes (row-major, same box).
 // --------------------------------------------------------------------------------------------------------------
-template <int PY, int PX, int IT, int CG>
+template <int PY, int PX, int IT, int CG, int PT>
 ICA_DEV void conv_up_x6w_class(const ConvParams& p, const f32x4* patch, int jt, int cb, int nch, int grp, long ps,
-                               f32x16 (&acc)[2][IT]) {
-  constexpr int PT = 2, KS = 5, PAD = 2, XU_PLANE = xu_plane<PT>();
+                               f32x16 (&acc)[PT][IT]) {
+  constexpr int KS = 5, PAD = 2, XU_PLANE = xu_plane<PT>();
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
   constexpr int NCG = CG / 16;
@@ -1184,19 +1085,18 @@ ICA_DEV void conv_up_x6w_class(const ConvParams& p, const f32x4* patch, int jt, 
   }
 }
 
-// GDN / IGDN backward epilogue of the 8-wave conv_up (two waves per SIMD, 256 registers): this wave's two pixel
-// tiles x IT * 32 channels (all of Cout).  The wide form's t (IT * 16 registers) and 2x (IT * 16) do not fit next
-// to both tiles' accumulators, so t goes through this wave's LDS slab (4 IT x 64 entries: the block's LDS, free
-// after the barrier that ends every wave's main loop) and 2x is formed again when it is used:
-//   pass 1 (per channel tile it): the saved (y, s) quads -> t into the slab (k-step order), g*s in place of g;
-//   pass 2 (per output tile jt): the (y, s) quads of jt re-read (issued before the GEMM: the SIMD partner's MFMAs
-//   cover the latency), u = gamma'^T t on x6 MFMAs over the k-steps of the slab (each split on the fly), and
-//   dx = g*s + 2 y rcp(s) u.
-// Pass 1's (y, s) quads run in a two-channel-tile ring (64 registers): the first two tiles' loads of pixel tile 0
-// are issued before the block barrier (gdn_bwd_x6w_pre), so a wave that ends its main loop early spends the wait on
-// them, and each later tile's loads go out two tiles ahead of their use.
-// Every output gets the arithmetic and MFMA order of gdn_bwd_x6_wide; the saved (y, s) are read twice (the second
-// time mostly from L2 / the MALL).
+// GDN / IGDN backward epilogue of the 8-wave conv_up (two waves per SIMD, 256 registers): this wave's PT pixel
+// tiles x IT * 32 channels (all of Cout).  The wide form keeps t (IT * 16 registers) and 2x (IT * 16) beside the
+// accumulators, which does not fit at 256 registers; here t is parked in the wave's own region of the OUTPUT tensor
+// (the dx quads it will overwrite at the end: a same-lane store, re-read, then overwrite, from L2), so the epilogue
+// needs no LDS and no block barrier: a wave starts it as soon as its own main loop ends.  The SIMD's arbiter favours
+// the older wave (waves w and w + 4 share a SIMD; stamped: waves 0-3 end their main loops 40-80k cycles before
+// 4-7), so the kernel gives waves 0-3 the shorter classes and their epilogues run under the partners' MFMAs.
+//   pass 1 (per channel tile it): the saved (y, s) quads (a two-tile ring, the first two issued as the main loop
+//   ends) -> t into the parked output quads, g*s in place of g (PT = 1: 2x kept in registers as well);
+//   pass 2: u = gamma'^T t for every output tile (x6 MFMAs in two halves of IT / 2 tiles, t read back and split per
+//   k-step), then dx = g*s + 2x u over the parked t (PT = 2: 2x from the (y, s) quads read again).
+// Every output gets the arithmetic and MFMA order of gdn_bwd_x6_wide.
 struct X6wPix {
   unsigned vo[2], vl[2];
   bool valid[2];
@@ -1214,7 +1114,7 @@ ICA_DEV X6wPix x6w_pix(const ConvParams& p, const int (&oy)[2], const int (&ox)[
   }
   return r;
 }
-// the (y, s) quads of channel tile it of pixel tile t (vl: x6w_pix)
+// the (y, s) quads of channel tile it at lane offset vl (x6w_pix)
 ICA_DEV void x6w_ys(const ConvParams& p, int n, unsigned vl, int it, f32x4 (&yq)[4], f32x4 (&sq)[4]) {
   const unsigned plane = (unsigned)p.Hout * p.Wout;
   const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
@@ -1226,23 +1126,20 @@ ICA_DEV void x6w_ys(const ConvParams& p, int n, unsigned vl, int it, f32x4 (&yq)
   }
 }
 
-template <int IT, int EPI>
-ICA_DEV void gdn_bwd_x6w_slab(const ConvParams& p, f32x16 (&acc)[2][IT], int n, const X6wPix& px,
-                              f32x4 (&ry)[2][4], f32x4 (&rs)[2][4], f32x4* slab) {
+template <int IT, int EPI, int PT>
+ICA_DEV void gdn_bwd_x6w_park(const ConvParams& p, f32x16 (&acc)[PT][IT], int n, const X6wPix& px,
+                              f32x4 (&ry)[2][4], f32x4 (&rs)[2][4]) {
   static_assert(EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD, "GDN backward epilogues only");
-  static_assert(IT >= 2, "x6w GDN backward: a two-tile (y, s) ring");
+  static_assert(IT >= 2 && IT % 2 == 0, "x6w GDN backward: a two-tile (y, s) ring, u in two halves");
+  constexpr int H2 = IT / 2;
   const int lane = threadIdx.x & 63;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
   const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
   const Img4 Y(p.y, img, n);
   const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
-  auto ldg = [&](bf16x8 (&a)[3], int jt, int k) {
+  f32x16 xx[PT == 1 ? IT : 1];
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      a[q] = ld_bf8(grs, lane * 16, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
-  };
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < PT; ++t) {
     if (t == 1) {   // pixel tile 1: its ring starts here
       x6w_ys(p, n, px.vl[1], 0, ry[0], rs[0]);
       x6w_ys(p, n, px.vl[1], 1, ry[1], rs[1]);
@@ -1259,41 +1156,59 @@ ICA_DEV void gdn_bwd_x6w_slab(const ConvParams& p, f32x16 (&acc)[2][IT], int n, 
           const float gx = acc[t][it][4 * g + e] * xs;
           tv[e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : (0.5f * gx) * rc;
           float gs = acc[t][it][4 * g + e] * sg;
-          asm volatile("" : "+v"(gs));   // g*s rounded on its own: never contracted into dx's fma
+          float x2 = 2.0f * xs;
+          asm volatile("" : "+v"(gs), "+v"(x2));   // rounded on their own: never contracted into dx's fma
           acc[t][it][4 * g + e] = gs;
+          if constexpr (PT == 1) xx[it][4 * g + e] = x2;
         }
-        slab[((2 * it + (g >> 1)) * 2 + (g & 1)) * 64 + lane] = tv;   // k-step 2 it + g / 2, half g & 1
+        if (px.valid[t]) Y.st(px.vo[t], (unsigned)(it * 8 + 2 * g) * plane, tv);   // parked t
       }
       if (it + 2 < IT) x6w_ys(p, n, px.vl[t], it + 2, ry[it & 1], rs[it & 1]);
+    }
+    f32x16 ux[IT];
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+      for (int j2 = 0; j2 < H2; ++j2) ux[hb * H2 + j2] = f32x16{0};
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 ga[H2][3];
+#pragma unroll
+        for (int j2 = 0; j2 < H2; ++j2)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            ga[j2][q] = ld_bf8(grs, lane * 16,
+                               ((((hb * H2 + j2) * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+        // k-step k: channel tile k / 2, register quads 2 (k & 1), 2 (k & 1) + 1 of this lane's pixel
+        const unsigned c0 = (unsigned)((k >> 1) * 8 + 4 * (k & 1)) * plane;
+        const f32x4 a = Y.ld(px.vl[t], c0), b = Y.ld(px.vl[t], c0 + 2 * plane);
+        const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        bf16x8 tq[3];
+        split3x8(v, tq);
+#pragma unroll
+        for (int j2 = 0; j2 < H2; ++j2) ux[hb * H2 + j2] = mfma_x6(ga[j2], tq, ux[hb * H2 + j2]);
+      }
     }
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) {
       __builtin_amdgcn_sched_barrier(0);
       f32x4 yq[4], sq[4];
-      x6w_ys(p, n, px.vl[t], jt, yq, sq);
-      f32x16 ux = f32x16{0};
-      bf16x8 ga[2][3];
-      ldg(ga[0], jt, 0);
-#pragma unroll
-      for (int k = 0; k < 2 * IT; ++k) {
-        if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], jt, k + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        const f32x4 a = slab[(2 * k) * 64 + lane], b = slab[(2 * k + 1) * 64 + lane];
-        const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-        bf16x8 tq[3];
-        split3x8(v, tq);
-        ux = mfma_x6(ga[k & 1], tq, ux);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PT != 1) x6w_ys(p, n, px.vl[t], jt, yq, sq);
       if (px.valid[t]) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           f32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float x2 = 2.0f * (yq[g][e] * __builtin_amdgcn_rcpf(sq[g][e]));
-            asm volatile("" : "+v"(x2));   // as in the wide form: 2x materialised, then one fma with u
-            o[e] = acc[t][jt][4 * g + e] + x2 * ux[4 * g + e];
+            float x2;
+            if constexpr (PT == 1) {
+              x2 = xx[jt][4 * g + e];
+            } else {
+              x2 = 2.0f * (yq[g][e] * __builtin_amdgcn_rcpf(sq[g][e]));
+              asm volatile("" : "+v"(x2));   // as in the wide form: 2x materialised, then one fma with u
+            }
+            o[e] = acc[t][jt][4 * g + e] + x2 * ux[jt][4 * g + e];
           }
           Y.st(px.vo[t], (unsigned)(jt * 8 + 2 * g) * plane, o);
         }
@@ -1303,10 +1218,10 @@ ICA_DEV void gdn_bwd_x6w_slab(const ConvParams& p, f32x16 (&acc)[2][IT], int n, 
   }
 }
 
-template <int IT, int EPI, int CG>
+template <int IT, int EPI, int CG, int PT = 2>
 __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long ps) {
   ICA_STAMP_BEGIN();
-  constexpr int PT = 2, NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
+  constexpr int NQ = CG / 4, XU_TH = xu_th<PT>(), XU_PLANE = xu_plane<PT>();
   extern __shared__ f32x4 patch[];   // [plane][CG/8][XU_PLANE]
   const int tiles_x = (p.Win + XU_TW - 1) / XU_TW, tiles_y = (p.Hin + XU_TH - 1) / XU_TH;
   int bid, cb;
@@ -1364,10 +1279,14 @@ __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long 
       for (int it = 0; it < IT; ++it) acc[t][it] = f32x16{0};
     for (int grp = 0; grp < ngrp; ++grp) {
       if (refill) fill(grp);
-      conv_up_x6w_class<PY, PX, IT, CG>(p, patch, jt, cb, nch, grp, ps, acc);
+      conv_up_x6w_class<PY, PX, IT, CG, PT>(p, patch, jt, cb, nch, grp, ps, acc);
     }
-    const int oy[2] = {2 * (a0 + a_rel) + PY, 2 * (a0 + a_rel + 2) + PY};
-    const int ox[2] = {2 * (b0 + b_rel) + PX, 2 * (b0 + b_rel) + PX};
+    int oy[2], ox[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {   // (PT = 1 uses entry 0 only)
+      oy[t] = 2 * (a0 + a_rel + 2 * t) + PY;
+      ox[t] = 2 * (b0 + b_rel) + PX;
+    }
     static_assert(EPI == EPI_BIAS || EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD ||
                       EPI == EPI_IGDN_BWD, "conv_up_x6w: bias, GDN / IGDN and their backward epilogues");
     if constexpr (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) {
@@ -1376,9 +1295,8 @@ __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long 
       x6w_ys(p, n, px.vl[0], 0, ry[0], rs[0]);
       x6w_ys(p, n, px.vl[0], 1, ry[1], rs[1]);
       ICA_STAMP_AT(0);
-      __syncthreads();   // every wave's main loop is done with the patch: the LDS becomes the waves' t slabs
-      ICA_STAMP_AT(1);
-      gdn_bwd_x6w_slab<IT, EPI>(p, acc, n, px, ry, rs, patch + wave * (4 * IT * 64));
+      ICA_STAMP_WAVE();
+      gdn_bwd_x6w_park<IT, EPI, PT>(p, acc, n, px, ry, rs);
     } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
 #pragma unroll
       for (int t = 0; t < PT; ++t) gdn_fwd_x6_tile_narrow<IT, EPI>(p, acc[t], n, oy[t], ox[t]);
@@ -1394,8 +1312,10 @@ __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long 
   const bool multi = ngrp > 1;
   if (!multi) fill(0);
   // SIMD partners (w, w + 4): (0,0) 9 taps with (1,1) 4 taps; (0,1) with (1,0), 6 + 6.  Every wave joins every
-  // fill barrier (one class each, the same group sequence)
-  switch (wave >> 1) {
+  // fill barrier (one class each, the same group sequence).  The GDN backward gives the shorter class to the wave
+  // the SIMD's arbiter favours (w < 4), so that wave's epilogue runs under its partner's main loop
+  constexpr bool BWD = EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD;
+  switch ((wave >> 1) ^ (BWD ? 2 : 0)) {
     case 0: run_class(I0{}, I0{}, multi); break;
     case 1: run_class(I0{}, I1{}, multi); break;
     case 2: run_class(I1{}, I1{}, multi); break;
@@ -1958,15 +1878,6 @@ int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Wout + 31) / 32) * ((p.Hout + 3) / 4) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * 9 * IT * 64;
-#ifdef ICA_RGBW
-  if constexpr (IT == 4 && EPI != EPI_GDN_BWD) {   // A/B builds: the 8-wave form (ICA_RGBW = PT, 1 or 2)
-    constexpr int PT = ICA_RGBW;
-    const int tiles_w = ((p.Wout + 31) / 32) * ((p.Hout + 4 * PT - 1) / (4 * PT)) * p.N;
-    ICA_LAUNCH((conv_rgb_x6w_kernel<EPI, PT>), dim3(tiles_w, ncb), dim3(512), 0, st, p, ps);
-    ICA_CHECK_LAUNCH();
-    return 0;
-  }
-#endif
   if constexpr (EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD) {
     // one block per CU, a contiguous run of tiles each (the XCD-aware order keeps a run's halo rows in one L2)
     const int nblk = std::max(1, std::min(tiles, ica_cu_count() / ncb));
@@ -1998,23 +1909,20 @@ int launch_up_x6_pt(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
-template <int IT, int EPI, int CG>
+template <int IT, int EPI, int CG, int PT = 2>
 int launch_up_x6w(const ConvParams& p, hipStream_t st) {
-  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N;
+  const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<PT>() - 1) / xu_th<PT>()) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * 25 * (p.Cin / 16) * IT * 64;
-  // the GDN backward's t slabs (8 waves x 4 IT x 64 entries) reuse the patch LDS
-  constexpr bool BWD = EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD;
-  constexpr size_t slabs = BWD ? (size_t)8 * 4 * IT * 64 * sizeof(f32x4) : 0;
-  constexpr size_t lds = std::max((size_t)xu_lds_bytes<CG, 2>(), slabs);
+  constexpr size_t lds = xu_lds_bytes<CG, PT>();
   static_assert(lds <= 160 * 1024, "conv_up_x6w LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6w_kernel<IT, EPI, CG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6w_kernel<IT, EPI, CG, PT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  ICA_LAUNCH((conv_up_x6w_kernel<IT, EPI, CG>), dim3(tiles, ncb), dim3(512), lds, st, p, ps);
+  ICA_LAUNCH((conv_up_x6w_kernel<IT, EPI, CG, PT>), dim3(tiles, ncb), dim3(512), lds, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -2032,12 +1940,24 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
   const long ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long b2 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N * ncb;
   const long b1 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<1>() - 1) / xu_th<1>()) * p.N * ncb;
-  if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) return launch_up_x6_pt<IT, EPI, CG, 1>(p, st);
-  // the 8-wave class-per-wave kernel: forward layers (bias / IGDN) and, since round 5, the GDN backward with t in
-  // LDS slabs (gdn_bwd_x6w_slab; ICA_UP_BWD4 builds keep the 4-wave kernel's wide epilogue for A/B runs)
+  constexpr bool BWD = EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD;
+  if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) {
+#ifndef ICA_UP_BWD4
+    // the GDN backward's 8-wave kernel at PT = 1: the same bits as its PT = 2 form (a batch and its images alone
+    // may take different PT)
+    if constexpr (IT == 4 && BWD) return launch_up_x6w<IT, EPI, CG, 1>(p, st);
+#endif
+    return launch_up_x6_pt<IT, EPI, CG, 1>(p, st);
+  }
+  // the 8-wave class-per-wave kernel: forward layers (bias / IGDN) and, since round 5, the GDN backward with its t
+  // parked in the output (gdn_bwd_x6w_park; ICA_UP_BWD4 builds keep the 4-wave kernel's wide epilogue for A/B runs)
+#ifndef ICA_UPW_BWD_PT
+#define ICA_UPW_BWD_PT 2
+#endif
 #ifdef ICA_UP_BWD4
   if constexpr (EPI == EPI_BIAS || EPI == EPI_IGDN || EPI == EPI_GDN) return launch_up_x6w<IT, EPI, CG>(p, st);
 #else
+  if constexpr (IT == 4 && BWD) return launch_up_x6w<IT, EPI, CG, ICA_UPW_BWD_PT>(p, st);
   if constexpr (IT == 4) return launch_up_x6w<IT, EPI, CG>(p, st);
 #endif
   return launch_up_x6_pt<IT, EPI, CG, X6_PT>(p, st);

@@ -49,12 +49,23 @@ cases = {
     "up.gdn_bwd": (lambda: K.conv_up(x_lo, N, wc.bwd, None, N, K.EPI_GDN_BWD, gd, saved=(sx_hi, ss_hi),
                                      prec=wc.bwd_prec), flop + gflop),
 }
+if "--bf16" in sys.argv:   # config-5 shapes (8 x 2048^2: level 1 = 1024^2), bf16 kernels of ica_conv.hip (a
+    # -DICA_CLOCK_STAMP build of ica_conv.hip; phases: class A main / epilogue, class B main / epilogue)
+    BFT = torch.bfloat16
+    wcb = K.PackedConv(W1, b, "conv", 2, K.PREC_BF16)
+    x2b = K.empty_nc4(8, N, 512, 512, dev, BFT).uniform_(-1, 1)
+    y1b, s1b = K.empty_nc4(8, N, 1024, 1024, dev, BFT).uniform_(-1, 1), K.empty_nc4(8, N, 1024, 1024, dev, BFT).uniform_(0.5, 1)
+    fl5 = 2 * N * N * 25 * 512 * 512 * 8
+    cases = {"bf16 up.gdn_bwd 4w (config 5)": (lambda: K.conv_up(x2b, N, wcb.bwd, None, N, K.EPI_GDN_BWD, gd,
+                                                                  saved=(y1b, s1b), prec=1),
+                                               fl5 + 2 * N * N * 1024 * 1024 * 8)}
+    mfma_cycles = lambda fl: fl / (2 * 32 * 32 * 16) * 32   # noqa: E731  (one bf16 MFMA per 32x32x16)
 cases = {k: v for k, v in cases.items() if only in k}
 L = lib()
 L.ica_diag_stamp_buffer.argtypes = [ctypes.c_void_p, ctypes.c_uint]
 L.ica_diag_stamp_buffer.restype = ctypes.c_int
 slots = 1 << 16
-buf = torch.zeros(slots * 8, dtype=torch.int64, device=dev)
+buf = torch.zeros(slots * 16, dtype=torch.int64, device=dev)
 n_simd = torch.cuda.get_device_properties(dev).multi_processor_count * 4
 for name, (f, fl) in cases.items():
     assert L.ica_diag_stamp_buffer(None, 0) == 0
@@ -74,7 +85,9 @@ for name, (f, fl) in cases.items():
     f()
     torch.cuda.synchronize()
     assert L.ica_diag_stamp_buffer(None, 0) == 0
-    st = buf.view(-1, 8).cpu()
+    st16 = buf.view(-1, 16).cpu()
+    st16 = st16[st16[:, 7] > 0]
+    st = st16[:, :8]
     st = st[st[:, 7] > 0]
     dt, dr = (st[:, 6] - st[:, 0]).double(), (st[:, 7] - st[:, 1]).double()
     clk = (dt / dr * 100.0).tolist()            # MHz
@@ -99,3 +112,11 @@ for name, (f, fl) in cases.items():
         print("    wave-0 phases (median / mean cycles): " + ", ".join(
             f"{k} {v:.0f} / {m:.0f}" for k, v, m in zip(lab, d, mean)), flush=True)
     print(f"    block cycles mean {float(dt.mean()):.0f}, p90 {float(dt.quantile(0.9)):.0f}", flush=True)
+    wv = st16[:, 8:16]
+    if bool((wv > 0).any()):
+        rel = (wv - st16[:, :1]).double()
+        rel[wv == 0] = float("nan")
+        med = [float(rel[:, w][~rel[:, w].isnan()].median()) if bool((~rel[:, w].isnan()).any()) else float("nan")
+               for w in range(8)]
+        print("    per-wave stamp (median cycles after block entry): " + ", ".join(f"w{w} {m:.0f}" for w, m in
+                                                                               enumerate(med)), flush=True)
