@@ -878,6 +878,11 @@ ICA_DEV void conv_up_acc(const ConvParams& p, const f32x4* patch, int jt, int cb
   }
 }
 
+// the bf16 GDN-backward epilogue's (y, s) loads (conv_epilogue EAG): a two-channel-tile ring (ICA_UP_EAG=0 builds:
+// beside their use, the round-4 form, for A/B runs)
+#ifndef ICA_UP_EAG
+#define ICA_UP_EAG 2
+#endif
 // the epilogue of class (PY, PX) for the pixel tiles of row group jt
 template <int PY, int PX, int IT, int EPI, int FX, bool BF>
 ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], int n, int a0, int b0, int jt,
@@ -888,8 +893,8 @@ ICA_DEV void conv_up_store(const ConvParams& p, f32x16 (&acc)[up_pt<BF>()][IT], 
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
     const int oy = 2 * (a0 + a_rel + 2 * t) + PY, ox = 2 * (b0 + b_rel) + PX;
-    conv_epilogue<IT, EPI, FX, BF, 0, up_lg<IT, BF>(), false>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout,
-                                                          cb * IT * 32, lp);
+    conv_epilogue<IT, EPI, FX, BF, 0, up_lg<IT, BF>(), ICA_UP_EAG>(p, acc[t], n, oy, ox, oy < p.Hout && ox < p.Wout,
+                                                               cb * IT * 32, lp);
   }
 }
 

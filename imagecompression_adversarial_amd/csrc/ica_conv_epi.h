@@ -165,9 +165,12 @@ ICA_DEV unsigned pix_at(int y, int x, int H, int W, bool split) {
 // the three-plane gamma' pack of ica_pack_gdn_x6 (p.gp), fp32-accurate like the main loop of the x6 kernels.
 // LG: the epilogue parameters come from the block's epi_params_to_lds copy at lp (bf16 kernels); otherwise from
 // global memory
-// EAG (bf16 GDN backward): every (y, s) quad loaded before the first use (conv_down: igdn_bwd 2.17 -> 2.07 ms, RGB
-// igdn_bwd 2.01 -> 1.60 ms at the config-5 shapes); conv_up keeps the loads beside their use (3.43 vs 3.63 ms eager)
-template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false, bool EAG = true>
+// EAG (bf16 GDN backward): 1 = every (y, s) quad loaded before the first use (conv_down: igdn_bwd 2.17 -> 2.07 ms,
+// RGB igdn_bwd 2.01 -> 1.60 ms at the config-5 shapes); 2 = a two-channel-tile ring (32 registers: channel tile
+// it + 2's quads issued once tile it's are consumed), for conv_up at 252 registers, where the whole set measured
+// 3.43 -> 3.63 ms and loads beside their use compiled to one s_waitcnt vmcnt(0) per quad pair (16 HBM round trips
+// per tile, ~28k cycles per tile stamped at the config-5 shapes); 0 = beside their use
+template <int IT, int EPI, int FX, bool BF = false, int X6 = 0, bool LG = false, int EAG = 1>
 ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy, int ox,
                            bool valid, int co_base, const f32x4* lp = nullptr, float* lst = nullptr) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -452,8 +455,23 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
       const unsigned vo_ld = valid ? vo : 0x1FFFFFF0u;
       __builtin_amdgcn_sched_barrier(0);  // not into the main loop (its weight ring is live there)
       // EAG: every (y, s) quad of the tile in flight before the first use (raw 8-B bf16 quads: 64 registers at IT = 4)
-      u32x2 yq[EAG ? IT : 1][4], sq[EAG ? IT : 1][4];
-      if constexpr (EAG) {
+      u32x2 yq[EAG == 1 ? IT : 1][4], sq[EAG == 1 ? IT : 1][4];
+      u32x2 ry[EAG == 2 ? 2 : 1][4], rq[EAG == 2 ? 2 : 1][4];   // EAG 2: the two-tile ring
+      auto ring_ld = [&](int it) {
+        if constexpr (EAG == 2) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int so8 = (int)(so(it * 8 + 2 * g) * 8u);
+            ry[it & 1][g] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(IX.r, (int)(vo_ld * 8u), so8, 0));
+            rq[it & 1][g] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(IS.r, (int)(vo_ld * 8u), so8, 0));
+          }
+        }
+      };
+      if constexpr (EAG == 2) {
+        ring_ld(0);
+        if (IT > 1) ring_ld(1);
+      }
+      if constexpr (EAG == 1) {
 #pragma unroll
         for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -465,12 +483,14 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int it = 0; it < IT; ++it)
+      for (int it = 0; it < IT; ++it) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const unsigned ss = so(it * 8 + 2 * g);
-          const f32x4 yv = EAG ? bf4_to_f4(yq[EAG ? it : 0][g]) : IX.ld(vo_ld, ss);
-          const f32x4 sv = EAG ? bf4_to_f4(sq[EAG ? it : 0][g]) : IS.ld(vo_ld, ss);
+          const f32x4 yv = EAG == 1 ? bf4_to_f4(yq[EAG == 1 ? it : 0][g])
+                         : EAG == 2 ? bf4_to_f4(ry[EAG == 2 ? (it & 1) : 0][g]) : IX.ld(vo_ld, ss);
+          const f32x4 sv = EAG == 1 ? bf4_to_f4(sq[EAG == 1 ? it : 0][g])
+                         : EAG == 2 ? bf4_to_f4(rq[EAG == 2 ? (it & 1) : 0][g]) : IS.ld(vo_ld, ss);
           f32x4 x2;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -487,6 +507,10 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
           asm volatile("" : "+v"(q));
           x2q[it][g] = q;
         }
+        if constexpr (EAG == 2) {
+          if (it + 2 < IT) ring_ld(it + 2);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);  // pack 2x here, do not sink y and rcp(s) into the second phase
       const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 4096);
 #pragma unroll

@@ -1086,17 +1086,20 @@ ICA_DEV void conv_up_x6w_class(const ConvParams& p, const f32x4* patch, int jt, 
 }
 
 // GDN / IGDN backward epilogue of the 8-wave conv_up (two waves per SIMD, 256 registers): this wave's PT pixel
-// tiles x IT * 32 channels (all of Cout).  The wide form keeps t (IT * 16 registers) and 2x (IT * 16) beside the
-// accumulators, which does not fit at 256 registers; here t is parked in the wave's own region of the OUTPUT tensor
-// (the dx quads it will overwrite at the end: a same-lane store, re-read, then overwrite, from L2), so the epilogue
-// needs no LDS and no block barrier: a wave starts it as soon as its own main loop ends.  The SIMD's arbiter favours
-// the older wave (waves w and w + 4 share a SIMD; stamped: waves 0-3 end their main loops 40-80k cycles before
-// 4-7), so the kernel gives waves 0-3 the shorter classes and their epilogues run under the partners' MFMAs.
-//   pass 1 (per channel tile it): the saved (y, s) quads (a two-tile ring, the first two issued as the main loop
-//   ends) -> t into the parked output quads, g*s in place of g (PT = 1: 2x kept in registers as well);
-//   pass 2: u = gamma'^T t for every output tile (x6 MFMAs in two halves of IT / 2 tiles, t read back and split per
-//   k-step), then dx = g*s + 2x u over the parked t (PT = 2: 2x from the (y, s) quads read again).
-// Every output gets the arithmetic and MFMA order of gdn_bwd_x6_wide.
+// tiles x IT * 32 channels (all of Cout).  The wide form's t (IT * 16 registers) and 2x (IT * 16) do not fit next
+// to the accumulators, so t goes through this wave's LDS slab (4 IT x 64 entries: the block's LDS, free after the
+// barrier that ends every wave's main loop):
+//   pass 1 (per channel tile it): the saved (y, s) quads -> t into the slab (k-step order), g*s in place of g;
+//   pass 2 (per output tile jt): u = gamma'^T t on x6 MFMAs over the k-steps of the slab (each split on the fly),
+//   dx = g*s + 2x u.  PT = 2: 2x is formed again from the (y, s) quads of jt, re-read before the GEMM (the SIMD
+//   partner's MFMAs cover the latency); PT = 1 (64 accumulator registers): 2x is kept from pass 1, (y, s) read once.
+// Pass 1's (y, s) quads run in a two-channel-tile ring (64 registers): the first two tiles' loads of pixel tile 0
+// are issued before the block barrier, which waits for LDS operations only (barrier_lds_only), so they stay in
+// flight through it; each later tile's loads go out two tiles ahead of their use.
+// Every output gets the arithmetic and MFMA order of gdn_bwd_x6_wide, at PT = 1 and 2 alike.
+// Measured and not kept (profiles/r05): t parked in the output tensor instead of LDS, no barrier, the shorter classes
+// on the waves the SIMD arbiter favours (so their epilogues run under the partners' main loops): 4.23 -> 5.14 ms, the
+// early epilogues' memory traffic delayed the partners' weight loads (their main loops ended 70k cycles later).
 struct X6wPix {
   unsigned vo[2], vl[2];
   bool valid[2];
@@ -1127,16 +1130,20 @@ ICA_DEV void x6w_ys(const ConvParams& p, int n, unsigned vl, int it, f32x4 (&yq)
 }
 
 template <int IT, int EPI, int PT>
-ICA_DEV void gdn_bwd_x6w_park(const ConvParams& p, f32x16 (&acc)[PT][IT], int n, const X6wPix& px,
-                              f32x4 (&ry)[2][4], f32x4 (&rs)[2][4]) {
+ICA_DEV void gdn_bwd_x6w_slab(const ConvParams& p, f32x16 (&acc)[PT][IT], int n, const X6wPix& px,
+                              f32x4 (&ry)[2][4], f32x4 (&rs)[2][4], f32x4* slab) {
   static_assert(EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD, "GDN backward epilogues only");
-  static_assert(IT >= 2 && IT % 2 == 0, "x6w GDN backward: a two-tile (y, s) ring, u in two halves");
-  constexpr int H2 = IT / 2;
+  static_assert(IT >= 2, "x6w GDN backward: a two-tile (y, s) ring");
   const int lane = threadIdx.x & 63;
   const unsigned plane = (unsigned)p.Hout * p.Wout;
   const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
   const Img4 Y(p.y, img, n);
   const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(p.gp, IT * IT * 6144);
+  auto ldg = [&](bf16x8 (&a)[3], int jt, int k) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      a[q] = ld_bf8(grs, lane * 16, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
+  };
   f32x16 xx[PT == 1 ? IT : 1];
 #pragma unroll
   for (int t = 0; t < PT; ++t) {
@@ -1161,40 +1168,29 @@ ICA_DEV void gdn_bwd_x6w_park(const ConvParams& p, f32x16 (&acc)[PT][IT], int n,
           acc[t][it][4 * g + e] = gs;
           if constexpr (PT == 1) xx[it][4 * g + e] = x2;
         }
-        if (px.valid[t]) Y.st(px.vo[t], (unsigned)(it * 8 + 2 * g) * plane, tv);   // parked t
+        slab[((2 * it + (g >> 1)) * 2 + (g & 1)) * 64 + lane] = tv;   // k-step 2 it + g / 2, half g & 1
       }
       if (it + 2 < IT) x6w_ys(p, n, px.vl[t], it + 2, ry[it & 1], rs[it & 1]);
-    }
-    f32x16 ux[IT];
-#pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
-#pragma unroll
-      for (int j2 = 0; j2 < H2; ++j2) ux[hb * H2 + j2] = f32x16{0};
-#pragma unroll
-      for (int k = 0; k < 2 * IT; ++k) {
-        __builtin_amdgcn_sched_barrier(0);
-        bf16x8 ga[H2][3];
-#pragma unroll
-        for (int j2 = 0; j2 < H2; ++j2)
-#pragma unroll
-          for (int q = 0; q < 3; ++q)
-            ga[j2][q] = ld_bf8(grs, lane * 16,
-                               ((((hb * H2 + j2) * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + q * IT * IT * 2048);
-        // k-step k: channel tile k / 2, register quads 2 (k & 1), 2 (k & 1) + 1 of this lane's pixel
-        const unsigned c0 = (unsigned)((k >> 1) * 8 + 4 * (k & 1)) * plane;
-        const f32x4 a = Y.ld(px.vl[t], c0), b = Y.ld(px.vl[t], c0 + 2 * plane);
-        const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-        bf16x8 tq[3];
-        split3x8(v, tq);
-#pragma unroll
-        for (int j2 = 0; j2 < H2; ++j2) ux[hb * H2 + j2] = mfma_x6(ga[j2], tq, ux[hb * H2 + j2]);
-      }
     }
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) {
       __builtin_amdgcn_sched_barrier(0);
       f32x4 yq[4], sq[4];
       if constexpr (PT != 1) x6w_ys(p, n, px.vl[t], jt, yq, sq);
+      f32x16 ux = f32x16{0};
+      bf16x8 ga[2][3];
+      ldg(ga[0], jt, 0);
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], jt, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x4 a = slab[(2 * k) * 64 + lane], b = slab[(2 * k + 1) * 64 + lane];
+        const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        bf16x8 tq[3];
+        split3x8(v, tq);
+        ux = mfma_x6(ga[k & 1], tq, ux);
+      }
+      __builtin_amdgcn_sched_barrier(0);
       if (px.valid[t]) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -1208,7 +1204,7 @@ ICA_DEV void gdn_bwd_x6w_park(const ConvParams& p, f32x16 (&acc)[PT][IT], int n,
               x2 = 2.0f * (yq[g][e] * __builtin_amdgcn_rcpf(sq[g][e]));
               asm volatile("" : "+v"(x2));   // as in the wide form: 2x materialised, then one fma with u
             }
-            o[e] = acc[t][jt][4 * g + e] + x2 * ux[jt][4 * g + e];
+            o[e] = acc[t][jt][4 * g + e] + x2 * ux[4 * g + e];
           }
           Y.st(px.vo[t], (unsigned)(jt * 8 + 2 * g) * plane, o);
         }
@@ -1216,6 +1212,12 @@ ICA_DEV void gdn_bwd_x6w_park(const ConvParams& p, f32x16 (&acc)[PT][IT], int n,
     }
     ICA_STAMP_AT(2 + t);
   }
+}
+
+// a block barrier that waits only for this wave's LDS operations (the waves' patch reads), not for its global loads:
+// the (y, s) loads issued before it stay in flight through the wait
+ICA_DEV void barrier_lds_only() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int IT, int EPI, int CG, int PT = 2>
@@ -1296,7 +1298,9 @@ __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long 
       x6w_ys(p, n, px.vl[0], 1, ry[1], rs[1]);
       ICA_STAMP_AT(0);
       ICA_STAMP_WAVE();
-      gdn_bwd_x6w_park<IT, EPI, PT>(p, acc, n, px, ry, rs);
+      barrier_lds_only();   // every wave's main loop is done with the patch: the LDS becomes the waves' t slabs
+      ICA_STAMP_AT(1);
+      gdn_bwd_x6w_slab<IT, EPI, PT>(p, acc, n, px, ry, rs, patch + wave * (4 * IT * 64));
     } else if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
 #pragma unroll
       for (int t = 0; t < PT; ++t) gdn_fwd_x6_tile_narrow<IT, EPI>(p, acc[t], n, oy[t], ox[t]);
@@ -1312,10 +1316,8 @@ __global__ __launch_bounds__(512, 1) void conv_up_x6w_kernel(ConvParams p, long 
   const bool multi = ngrp > 1;
   if (!multi) fill(0);
   // SIMD partners (w, w + 4): (0,0) 9 taps with (1,1) 4 taps; (0,1) with (1,0), 6 + 6.  Every wave joins every
-  // fill barrier (one class each, the same group sequence).  The GDN backward gives the shorter class to the wave
-  // the SIMD's arbiter favours (w < 4), so that wave's epilogue runs under its partner's main loop
-  constexpr bool BWD = EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD;
-  switch ((wave >> 1) ^ (BWD ? 2 : 0)) {
+  // fill barrier (one class each, the same group sequence)
+  switch (wave >> 1) {
     case 0: run_class(I0{}, I0{}, multi); break;
     case 1: run_class(I0{}, I1{}, multi); break;
     case 2: run_class(I1{}, I1{}, multi); break;
@@ -1914,7 +1916,10 @@ int launch_up_x6w(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<PT>() - 1) / xu_th<PT>()) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
   const long ps = (long)ncb * 25 * (p.Cin / 16) * IT * 64;
-  constexpr size_t lds = xu_lds_bytes<CG, PT>();
+  // the GDN backward's t slabs (8 waves x 4 IT x 64 entries) reuse the patch LDS
+  constexpr bool BWD = EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD;
+  constexpr size_t slabs = BWD ? (size_t)8 * 4 * IT * 64 * sizeof(f32x4) : 0;
+  constexpr size_t lds = std::max((size_t)xu_lds_bytes<CG, PT>(), slabs);
   static_assert(lds <= 160 * 1024, "conv_up_x6w LDS");
   static bool attr_set = false;
   if (!attr_set) {
@@ -1949,8 +1954,8 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
 #endif
     return launch_up_x6_pt<IT, EPI, CG, 1>(p, st);
   }
-  // the 8-wave class-per-wave kernel: forward layers (bias / IGDN) and, since round 5, the GDN backward with its t
-  // parked in the output (gdn_bwd_x6w_park; ICA_UP_BWD4 builds keep the 4-wave kernel's wide epilogue for A/B runs)
+  // the 8-wave class-per-wave kernel: forward layers (bias / IGDN) and, since round 5, the GDN backward with t in LDS
+  // slabs (gdn_bwd_x6w_slab; ICA_UP_BWD4 builds keep the 4-wave kernel's wide epilogue for A/B runs)
 #ifndef ICA_UPW_BWD_PT
 #define ICA_UPW_BWD_PT 2
 #endif
