@@ -61,6 +61,10 @@ ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
 // L1 -> register stream of 4 KB per wave-step, the bf16 main loop's limit) feeds twice the MFMAs
 template <int CC, bool BF>
 constexpr int down_pt() { return (BF && CC == 16) ? 2 : 1; }
+// the x6 k3 conv_down at two rows per wave for the non-GDN layers (ICA_X6O_PT2=0 builds: one row, for A/B runs)
+#ifndef ICA_X6O_PT2
+#define ICA_X6O_PT2 1
+#endif
 
 // occupancy target: 2 blocks/CU, except the k5 IT = 6 (C = 192, bmshj2018 q6-8) variants, whose 6-tile
 // accumulators + fragment ring + GDN epilogue need the whole 512-register file (1 block/CU, no spills)
@@ -78,9 +82,11 @@ constexpr int conv_down_waves() {
 // three-plane weight pack of ica_pack_conv_weight_x6, six MFMAs per 16-deep k step; x6 GDN epilogue GEMMs on the
 // ica_pack_gdn_x6 pack): the k3 s1 layers of cheng2020 on the x6 ceiling.  One block per CU (512 registers); two for
 // IT = 1 (g_s.7's 16 rho rows: 16 accumulators).
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false>
+// XPT: 32-px rows per wave on the X6O path (2 only for the non-GDN epilogues at IT >= 4, see pick_tw_down_x6o).
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1>
 __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
-  constexpr int PT = down_pt<CC, BF>();
+  constexpr int PT = X6O ? XPT : down_pt<CC, BF>();
+  static_assert(XPT == 1 || (X6O && XPT == 2 && !epi_gdn<EPI>() && IT >= 4), "x6 conv_down: two rows per wave only without a GDN epilogue");
   constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
   constexpr int NQ = CC / 4, KH = CC / 2, PLANE = PR * PC, PAD = KS / 2;
@@ -525,34 +531,86 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
 #pragma unroll
     for (int i = 0; i < NF; ++i) fput(patch, i);
     __syncthreads();
-    bf16x8 fr[3][IT][3];
-    ldw(fr[0], 0);
-    ldw(fr[1], 1);
-#pragma unroll 1
-    for (int ch = 0; ch < nch; ++ch) {
-      const f32x4* cur = patch + (ch & 1) * 6 * PLANE;
-      f32x4* nxt = patch + ((ch & 1) ^ 1) * 6 * PLANE;
-      // B operands: tap t + 1's three planes are read during tap t (tap 0's right after the barrier)
-      bf16x8 bb[2][3];
-      auto ldb = [&](bf16x8 (&b)[3], int tap) {
-        const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-        const int o = h * PLANE + lbase + ky * PC + kx;
-        b[0] = f4_as_bf8(cur[o]);
-        b[1] = f4_as_bf8(cur[2 * PLANE + o]);
-        b[2] = f4_as_bf8(cur[4 * PLANE + o]);
+    if constexpr (PT == 2) {
+      // Two 32-px rows per wave (the non-GDN k3 layers on large grids): each weight fragment -- the main loop's
+      // L1 -> register stream, ~37 B/cycle/CU at one row -- feeds twice the MFMAs.  The 2 x IT accumulators leave
+      // room for two weight sets only, so the ring is a ping-pong one tap ahead; KK is odd, so a chunk's first set
+      // is ch & 1 and the loop body runs a chunk pair.  A tap's fill load is issued after the next tap's weights,
+      // so the in-order vmcnt waits on it only at its own split PUTD taps later.  Same MFMA order per output as
+      // PT = 1 (bit-identical results).
+      static_assert(KK % 2 == 1, "x6 conv_down ping-pong: KK odd");
+      bf16x8 fr[2][IT][3];
+      ldw(fr[0], 0);
+      auto chunk = [&](int ch, auto r0) {
+        constexpr int R0 = decltype(r0)::value;
+        const f32x4* cur = patch + (ch & 1) * 6 * PLANE;
+        f32x4* nxt = patch + ((ch & 1) ^ 1) * 6 * PLANE;
+        bf16x8 bb[2][PT][3];
+        auto ldb = [&](bf16x8 (&b)[PT][3], int tap) {
+          const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+#pragma unroll
+          for (int t = 0; t < PT; ++t) {
+            const int o = h * PLANE + lb[t] + ky * PC + kx;
+            b[t][0] = f4_as_bf8(cur[o]);
+            b[t][1] = f4_as_bf8(cur[2 * PLANE + o]);
+            b[t][2] = f4_as_bf8(cur[4 * PLANE + o]);
+          }
+        };
+        ldb(bb[0], 0);
+#pragma unroll
+        for (int tap = 0; tap < KK; ++tap) {
+          ldw(fr[(R0 + tap + 1) & 1], ch * KK + tap + 1);
+          if (tap < NF) fload(ch + 1, tap);
+          if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
+          if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int t = 0; t < PT; ++t)
+              acc[t][it] = mfma_x6(fr[(R0 + tap) & 1][it], bb[tap & 1][t], acc[t][it]);
+        }
+        __syncthreads();
       };
-      ldb(bb[0], 0);
-#pragma unroll
-      for (int tap = 0; tap < KK; ++tap) {
-        ldw(fr[(tap + 2) % 3], ch * KK + tap + 2);
-        if (tap < NF) fload(ch + 1, tap);   // past the last chunk: c4 >= Cin4, zero reads into the idle buffer
-        if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
-        if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(fr[tap % 3][it], bb[tap & 1], acc[0][it]);
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      int ch = 0;
+#pragma unroll 1
+      for (; ch + 1 < nch; ch += 2) {
+        chunk(ch, I0{});
+        chunk(ch + 1, I1{});
       }
-      __syncthreads();
+      if (ch < nch) chunk(ch, I0{});
+    } else {
+      bf16x8 fr[3][IT][3];
+      ldw(fr[0], 0);
+      ldw(fr[1], 1);
+  #pragma unroll 1
+      for (int ch = 0; ch < nch; ++ch) {
+        const f32x4* cur = patch + (ch & 1) * 6 * PLANE;
+        f32x4* nxt = patch + ((ch & 1) ^ 1) * 6 * PLANE;
+        // B operands: tap t + 1's three planes are read during tap t (tap 0's right after the barrier)
+        bf16x8 bb[2][3];
+        auto ldb = [&](bf16x8 (&b)[3], int tap) {
+          const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+          const int o = h * PLANE + lbase + ky * PC + kx;
+          b[0] = f4_as_bf8(cur[o]);
+          b[1] = f4_as_bf8(cur[2 * PLANE + o]);
+          b[2] = f4_as_bf8(cur[4 * PLANE + o]);
+        };
+        ldb(bb[0], 0);
+  #pragma unroll
+        for (int tap = 0; tap < KK; ++tap) {
+          ldw(fr[(tap + 2) % 3], ch * KK + tap + 2);
+          if (tap < NF) fload(ch + 1, tap);   // past the last chunk: c4 >= Cin4, zero reads into the idle buffer
+          if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
+          if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
+          __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+          for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(fr[tap % 3][it], bb[tap & 1], acc[0][it]);
+        }
+        __syncthreads();
+      }
     }
   } else {
     // Weight fragments stream linearly through (chunk, tap); they are prefetched
@@ -1684,12 +1742,12 @@ constexpr bool down_variant() {
 template <int KS, int S>
 constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) || (KS == 1 && S == 2); }
 
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1>
 static int launch_down(const ConvParams& p, hipStream_t st) {
-  constexpr int TH = down_pt<CC, BF>() * 128 / TW;
+  constexpr int TH = (X6O ? XPT : down_pt<CC, BF>()) * 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  ICA_LAUNCH((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O>), grid, dim3(256), 0, st, p);
+  ICA_LAUNCH((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O, XPT>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1702,6 +1760,17 @@ static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
   if constexpr (!down_variant<3, 1, IT, EPI, FX>()) {
     return -4;
   } else {
+    // two rows per wave (half the weight-fragment stream per MFMA) where the halved grid still gives every CU
+    // >= 4 blocks; the GDN epilogues keep one (their normaliser GEMMs need the registers)
+    if constexpr (ICA_X6O_PT2 && !epi_gdn<EPI>() && IT >= 4) {
+      const int cbs = (p.Cout + IT * 32 - 1) / (IT * 32);
+      if (p.Wout >= 32 && p.Wout % 32 == 0) {
+        if ((long)(p.Wout / 32) * ((p.Hout + 7) / 8) * p.N * cbs >= 1024)
+          return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true, 2>(p, st);
+      } else if ((long)((p.Wout + 15) / 16) * ((p.Hout + 15) / 16) * p.N * cbs >= 1024) {
+        return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true, 2>(p, st);
+      }
+    }
     if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true>(p, st);
     return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true>(p, st);
   }

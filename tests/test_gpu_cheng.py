@@ -152,6 +152,54 @@ def test_subpel_shuffle_vs_torch(K, Cin, C, H, W, x6):
     assert rel_err(gx, xr.grad + r) < 1e-4
 
 
+@pytest.mark.parametrize("H,W", [(130, 256), (136, 240)])
+def test_x6_k3_two_rows_per_wave_same_bits(K, H, W):
+    """The x6 k3 s1 conv_down runs two 32-px rows per wave (XPT = 2, ica_conv.hip pick_tw_down_x6o) for the non-GDN
+    epilogues once the halved grid still holds >= 1024 blocks, one row below that.  Same MFMA order per output, so an
+    8-image batch (two rows) must give image 0's and image 7's bits exactly as the 1-image launches (one row) -- which
+    the small-shape x6 tests pin against float64 -- for every fill / epilogue the two-row kernel serves: bias, leaky
+    ReLU + residual + saved activation, masked leaky-ReLU backward, PixelShuffle forward (bias, leaky ReLU),
+    PixelUnshuffle input gradient (+ residual).  Row tiles cut by the image bottom (H % 8, H % 16), 16-px-wide tiles
+    at W = 240; plus an fp32-tolerance check of the batch against torch."""
+    from imagecompression_adversarial_amd.engine_cheng import Conv3, Subpel
+    C, N = 192, 8
+    g = torch.Generator(device=DEV).manual_seed(40)
+
+    def r(*shape, s=1.0):
+        return (torch.rand(shape, generator=g, device=DEV) * 2 - 1) * s
+
+    w, b = r(C, C, 3, 3, s=(C * 9) ** -0.5), r(C, s=0.1)
+    cv = Conv3(w, b, 1, x6=True)
+    ws, bs = r(4 * C, C, 3, 3, s=(C * 9) ** -0.5), r(4 * C, s=0.1)
+    sp = Subpel(ws, bs, x6=True)
+    assert cv.fwd6 is not None and cv.bwd6 is not None and sp.fwd6 is not None and sp.bwd6 is not None
+    x, res, m1, m2 = (K.to_nc4(r(N, C, H, W)) for _ in range(4))
+    gps = K.to_nc4(r(N, C, 2 * H, 2 * W))
+
+    def runs(n0, n1):
+        sl = slice(n0, n1)
+        sv = torch.empty_like(x[sl])
+        out = {"bias": cv.forward(x[sl], K.EPI_BIAS),
+               "lrelu_res": cv.forward(x[sl], K.EPI_LRELU, res=res[sl], save_x=sv),
+               "lrelu_bwd": cv.dgrad(x[sl], K.EPI_LRELU_BWD, fill_mode=K.FILL_LRELU_MASK, mask=m2[sl],
+                                     saved=(m1[sl], None)),
+               "ps_bias": sp.forward(x[sl], K.EPI_BIAS), "ps_lrelu": sp.forward(x[sl], K.EPI_LRELU),
+               "unshuf": sp.dgrad(gps[sl]), "unshuf_res": sp.dgrad(gps[sl], res=res[sl])}
+        out["lrelu_saved"] = sv
+        return out
+
+    full = runs(0, N)
+    for n0 in (0, N - 1):
+        one = runs(n0, n0 + 1)
+        for k, v in one.items():
+            assert torch.equal(full[k][n0:n0 + 1], v), (k, n0)
+    xc = K.from_nc4(x[N - 1:], C).cpu()
+    ref = F.conv2d(xc, w.cpu(), b.cpu(), padding=1)
+    assert rel_err(K.from_nc4(full["bias"][N - 1:], C).cpu(), ref) < 1e-4
+    ref = lrelu(F.pixel_shuffle(F.conv2d(xc, ws.cpu(), bs.cpu(), padding=1), 2))
+    assert rel_err(K.from_nc4(full["ps_lrelu"][N - 1:], C).cpu(), ref) < 1e-4
+
+
 @pytest.mark.parametrize("x6", [False, True])
 @pytest.mark.parametrize("inverse", [False, True])
 def test_gdn_residual_fwd_bwd(K, inverse, x6):
