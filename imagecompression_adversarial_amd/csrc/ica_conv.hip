@@ -61,9 +61,13 @@ ICA_DEV void load_frag(float (&a)[IT][KH], const float* w) {
 // L1 -> register stream of 4 KB per wave-step, the bf16 main loop's limit) feeds twice the MFMAs
 template <int CC, bool BF>
 constexpr int down_pt() { return (BF && CC == 16) ? 2 : 1; }
-// the x6 k3 conv_down at two rows per wave for the non-GDN layers (ICA_X6O_PT2=0 builds: one row, for A/B runs)
+// the x6 k3 conv_down at two rows per wave on large grids (ICA_X6O_PT2=0 builds: one row; ICA_X6O_PT2_GDN=0: one row
+// for the GDN / IGDN (backward) epilogues -- for A/B runs)
 #ifndef ICA_X6O_PT2
 #define ICA_X6O_PT2 1
+#endif
+#ifndef ICA_X6O_PT2_GDN
+#define ICA_X6O_PT2_GDN 1
 #endif
 
 // occupancy target: 2 blocks/CU, except the k5 IT = 6 (C = 192, bmshj2018 q6-8) variants, whose 6-tile
@@ -82,11 +86,11 @@ constexpr int conv_down_waves() {
 // three-plane weight pack of ica_pack_conv_weight_x6, six MFMAs per 16-deep k step; x6 GDN epilogue GEMMs on the
 // ica_pack_gdn_x6 pack): the k3 s1 layers of cheng2020 on the x6 ceiling.  One block per CU (512 registers); two for
 // IT = 1 (g_s.7's 16 rho rows: 16 accumulators).
-// XPT: 32-px rows per wave on the X6O path (2 only for the non-GDN epilogues at IT >= 4, see pick_tw_down_x6o).
+// XPT: 32-px rows per wave on the X6O path (2 at IT >= 4 on large grids, see pick_tw_down_x6o).
 template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1>
 __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
   constexpr int PT = X6O ? XPT : down_pt<CC, BF>();
-  static_assert(XPT == 1 || (X6O && XPT == 2 && !epi_gdn<EPI>() && IT >= 4), "x6 conv_down: two rows per wave only without a GDN epilogue");
+  static_assert(XPT == 1 || (X6O && XPT == 2 && (ICA_X6O_PT2_GDN || !epi_gdn<EPI>()) && IT >= 4), "x6 conv_down: two rows per wave at IT >= 4");
   constexpr int TH = PT * 128 / TW;
   constexpr int PR = S * (TH - 1) + KS, PC = S * (TW - 1) + KS;
   constexpr int NQ = CC / 4, KH = CC / 2, PLANE = PR * PC, PAD = KS / 2;
@@ -532,7 +536,7 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
     for (int i = 0; i < NF; ++i) fput(patch, i);
     __syncthreads();
     if constexpr (PT == 2) {
-      // Two 32-px rows per wave (the non-GDN k3 layers on large grids): each weight fragment -- the main loop's
+      // Two 32-px rows per wave (the k3 layers on large grids): each weight fragment -- the main loop's
       // L1 -> register stream, ~37 B/cycle/CU at one row -- feeds twice the MFMAs.  The 2 x IT accumulators leave
       // room for two weight sets only, so the ring is a ping-pong one tap ahead; KK is odd, so a chunk's first set
       // is ch & 1 and the loop body runs a chunk pair.  A tap's fill load is issued after the next tap's weights,
@@ -1761,8 +1765,9 @@ static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
     return -4;
   } else {
     // two rows per wave (half the weight-fragment stream per MFMA) where the halved grid still gives every CU
-    // >= 4 blocks; the GDN epilogues keep one (their normaliser GEMMs need the registers)
-    if constexpr (ICA_X6O_PT2 && !epi_gdn<EPI>() && IT >= 4) {
+    // >= 4 blocks (k3 lrelu 9.66 -> 8.56 ms, gdn+res 12.05 -> 10.81 ms, gdn_bwd 12.2 -> 10.9 ms at the config-3
+    // shapes; the GDN epilogues run tile by tile, the second tile's accumulators held)
+    if constexpr (ICA_X6O_PT2 && (ICA_X6O_PT2_GDN || !epi_gdn<EPI>()) && IT >= 4) {
       const int cbs = (p.Cout + IT * 32 - 1) / (IT * 32);
       if (p.Wout >= 32 && p.Wout % 32 == 0) {
         if ((long)(p.Wout / 32) * ((p.Hout + 7) / 8) * p.N * cbs >= 1024)

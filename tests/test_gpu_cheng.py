@@ -154,13 +154,14 @@ def test_subpel_shuffle_vs_torch(K, Cin, C, H, W, x6):
 
 @pytest.mark.parametrize("H,W", [(130, 256), (136, 240)])
 def test_x6_k3_two_rows_per_wave_same_bits(K, H, W):
-    """The x6 k3 s1 conv_down runs two 32-px rows per wave (XPT = 2, ica_conv.hip pick_tw_down_x6o) for the non-GDN
-    epilogues once the halved grid still holds >= 1024 blocks, one row below that.  Same MFMA order per output, so an
-    8-image batch (two rows) must give image 0's and image 7's bits exactly as the 1-image launches (one row) -- which
-    the small-shape x6 tests pin against float64 -- for every fill / epilogue the two-row kernel serves: bias, leaky
-    ReLU + residual + saved activation, masked leaky-ReLU backward, PixelShuffle forward (bias, leaky ReLU),
-    PixelUnshuffle input gradient (+ residual).  Row tiles cut by the image bottom (H % 8, H % 16), 16-px-wide tiles
-    at W = 240; plus an fp32-tolerance check of the batch against torch."""
+    """The x6 k3 s1 conv_down runs two 32-px rows per wave (XPT = 2, ica_conv.hip pick_tw_down_x6o) once the halved
+    grid still holds >= 1024 blocks, one row below that.  Same MFMA order per output, so an 8-image batch (two rows)
+    must give image 0's and image 7's bits exactly as the 1-image launches (one row) -- which the small-shape x6 tests
+    pin against float64 -- for every fill / epilogue the two-row kernel serves: bias, leaky ReLU + residual + saved
+    activation, masked leaky-ReLU backward, PixelShuffle forward (bias, leaky ReLU), PixelUnshuffle input gradient
+    (+ residual), GDN / IGDN + residual forward (y, s saved) and their backward (residual gradient, summed gradient
+    saved).  Row tiles cut by the image bottom (H % 8, H % 16), 16-px-wide tiles at W = 240; plus an fp32-tolerance
+    check of the batch against torch."""
     from imagecompression_adversarial_amd.engine_cheng import Conv3, Subpel
     C, N = 192, 8
     g = torch.Generator(device=DEV).manual_seed(40)
@@ -173,19 +174,27 @@ def test_x6_k3_two_rows_per_wave_same_bits(K, H, W):
     ws, bs = r(4 * C, C, 3, 3, s=(C * 9) ** -0.5), r(4 * C, s=0.1)
     sp = Subpel(ws, bs, x6=True)
     assert cv.fwd6 is not None and cv.bwd6 is not None and sp.fwd6 is not None and sp.bwd6 is not None
+    P = oc.perturb_params({"t.beta": oc.gdn_init(C)[0], "t.gamma": oc.gdn_init(C)[1]}, seed=3)
+    gd = K.PackedGDN(P["t.beta"].to(DEV), P["t.gamma"].to(DEV))
     x, res, m1, m2 = (K.to_nc4(r(N, C, H, W)) for _ in range(4))
     gps = K.to_nc4(r(N, C, 2 * H, 2 * W))
 
     def runs(n0, n1):
         sl = slice(n0, n1)
-        sv = torch.empty_like(x[sl])
-        out = {"bias": cv.forward(x[sl], K.EPI_BIAS),
-               "lrelu_res": cv.forward(x[sl], K.EPI_LRELU, res=res[sl], save_x=sv),
-               "lrelu_bwd": cv.dgrad(x[sl], K.EPI_LRELU_BWD, fill_mode=K.FILL_LRELU_MASK, mask=m2[sl],
-                                     saved=(m1[sl], None)),
-               "ps_bias": sp.forward(x[sl], K.EPI_BIAS), "ps_lrelu": sp.forward(x[sl], K.EPI_LRELU),
-               "unshuf": sp.dgrad(gps[sl]), "unshuf_res": sp.dgrad(gps[sl], res=res[sl])}
-        out["lrelu_saved"] = sv
+        out = {"bias": cv.forward(x[sl], K.EPI_BIAS)}
+        sv = out["lrelu_saved"] = torch.empty_like(x[sl])
+        out["lrelu_res"] = cv.forward(x[sl], K.EPI_LRELU, res=res[sl], save_x=sv)
+        out["lrelu_bwd"] = cv.dgrad(x[sl], K.EPI_LRELU_BWD, fill_mode=K.FILL_LRELU_MASK, mask=m2[sl],
+                                    saved=(m1[sl], None))
+        out["ps_bias"] = sp.forward(x[sl], K.EPI_BIAS)
+        out["ps_lrelu"] = sp.forward(x[sl], K.EPI_LRELU)
+        out["unshuf"] = sp.dgrad(gps[sl])
+        out["unshuf_res"] = sp.dgrad(gps[sl], res=res[sl])
+        for inv, (ef, eb) in enumerate(((K.EPI_GDN, K.EPI_GDN_BWD), (K.EPI_IGDN, K.EPI_IGDN_BWD))):
+            yg, s, gs = (torch.empty_like(x[sl]) for _ in range(3))
+            out[f"gdn{inv}"] = cv.forward(x[sl], ef, gdn=gd, res=res[sl], save_x=yg, save_s=s)
+            out[f"gdn{inv}_bwd"] = cv.dgrad(m1[sl], eb, gdn=gd, res=m2[sl], save_x=gs, saved=(yg, s))
+            out[f"gdn{inv}_y"], out[f"gdn{inv}_s"], out[f"gdn{inv}_gsum"] = yg, s, gs
         return out
 
     full = runs(0, N)
