@@ -111,6 +111,8 @@ _SIGS = {
     "ica_relu_bwd": [_p, _p, _l, _p],
     "ica_abs_bwd": [_p, _p, _l, _p],
     "ica_gdn_xsq": [_p, _p, _p, _l, _p],
+    "ica_lrelu_bwd": [_p, _p, _p, _l, _p],
+    "ica_gdn_t": [_p, _p, _p, _p, _l, _i, _p],
     "ica_reparam_bwd": [_p, _p, _p, _l, _f, _i, _p],
     "ica_bpp_grad": [_p, _p, _l, _f, _p],
     "ica_gc_bwd": [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p],

@@ -830,7 +830,8 @@ def _ar_decompress(model, strings, shape):
 
 class Cheng2020Anchor(CompressionModel):
     """compressai.models.Cheng2020Anchor (JointAutoregressiveHierarchicalPriors with residual transforms).
-    Eval-mode forward (the attack path); training this model is out of scope."""
+    Eval-mode forward (the attack path) and the train-mode forward's values; the fine-tune's gradients come from
+    the HIP trainer (train_engine.RDTrainer -> train_cheng.ChengTrainStep, train.py --adv)."""
     model_kind = "cheng2020"
 
     def __init__(self, N=192, **kwargs):
@@ -848,7 +849,15 @@ class Cheng2020Anchor(CompressionModel):
 
     def forward(self, x):
         if self.training:
-            raise NotImplementedError("cheng2020 training is out of scope on the HIP path (eval forward only)")
+            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+                # no silent gradient hole (as _ForwardOnly): train through train_engine.RDTrainer
+                raise NotImplementedError("Cheng2020Anchor is forward-only on the module API; freeze it "
+                                          "(requires_grad_(False)) or train with train_engine.RDTrainer")
+            from .train_cheng import train_forward
+            sd = {k: v.detach() for k, v in self.state_dict().items()}
+            f = train_forward(self.kernels("fp32"), sd.__getitem__, K.to_nc4(x.detach().contiguous()))
+            return {"x_hat": K.from_nc4(f["xh4"], 3),
+                    "likelihoods": {"y": K.from_nc4(f["ylik4"], self.M), "z": K.from_nc4(f["zlik4"], self.N)}}
         res = self.kernels().forward(K.to_nc4(x.detach().contiguous()))
         return {"x_hat": K.from_nc4(res["x_hat4"], 3),
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}

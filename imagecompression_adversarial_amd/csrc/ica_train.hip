@@ -128,6 +128,27 @@ __global__ void abs_bwd_kernel(float* __restrict__ g, const float* __restrict__ 
   }
 }
 
+// leaky-ReLU backward into a separate tensor (the pre-activation gradient a weight gradient reads): a is the layer's
+// saved output (same sign as its input), slope 0.01 -- the same select as the conv fills / EPI_LRELU_BWD
+__global__ void lrelu_bwd_kernel(const float* __restrict__ g, const float* __restrict__ a, float* __restrict__ out,
+                                 long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = g[i];
+    out[i] = a[i] > 0.f ? v : v * 0.01f;
+  }
+}
+
+// t = dL/dn of a GDN / IGDN layer from g = dL/dy and its saved (y, s), y = x s:  GDN (s = n^-1/2) t = -0.5 g y s^2,
+// IGDN (s = n^1/2) t = 0.5 g y / s^2 -- the arithmetic of the fused GDN-backward epilogues (ica_conv_epi.h), for the
+// layers whose backward launch cannot write t (the k3 residual layers of cheng2020)
+__global__ void gdn_t_kernel(const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ s,
+                             float* __restrict__ t, long n, int inverse) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float sv = s[i], gy = g[i] * y[i];
+    t[i] = inverse ? (sv != 0.f ? 0.5f * gy / (sv * sv) : 0.f) : -0.5f * gy * (sv * sv);
+  }
+}
+
 // x^2 with x = y / s (GDN input recovered from the saved output y and s)
 __global__ void gdn_xsq_kernel(const float* __restrict__ y, const float* __restrict__ s, float* __restrict__ out,
                                long n) {
@@ -397,6 +418,12 @@ int ica_wgrad(const float* Sm, const float* Lg, float* ws, float* out, int N, in
     ICA_LAUNCH((wgrad_kernel<3, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
   else if (KS == 1 && S == 1)
     ICA_LAUNCH((wgrad_kernel<1, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
+  else if (KS == 3 && S == 2)   // cheng2020: the strided residual-block convs and h_a
+    ICA_LAUNCH((wgrad_kernel<3, 2>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
+  else if (KS == 1 && S == 2)   // cheng2020: the 1x1 stride-2 skips
+    ICA_LAUNCH((wgrad_kernel<1, 2>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
+  else if (KS == 5 && S == 1)   // the masked 5x5 context model (cheng2020, mbt2018)
+    ICA_LAUNCH((wgrad_kernel<5, 1>), grid, dim3(256), 0, st, Sm, Lg, ws, N, A, Bc, Hs, Ws_, Hb, Wb, P, nsplit);
   else
     return -6;
   ICA_CHECK_LAUNCH();
@@ -420,6 +447,18 @@ int ica_relu_bwd(float* g, const float* y, long n, hipStream_t st) {
 
 int ica_abs_bwd(float* g, const float* x, long n, hipStream_t st) {
   ICA_LAUNCH(abs_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, g, x, n);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_lrelu_bwd(const float* g, const float* a, float* out, long n, hipStream_t st) {
+  ICA_LAUNCH(lrelu_bwd_kernel, dim3(g1d(n)), dim3(256), 0, st, g, a, out, n);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
+int ica_gdn_t(const float* g, const float* y, const float* s, float* t, long n, int inverse, hipStream_t st) {
+  ICA_LAUNCH(gdn_t_kernel, dim3(g1d(n)), dim3(256), 0, st, g, y, s, t, n, inverse);
   ICA_CHECK_LAUNCH();
   return 0;
 }

@@ -189,10 +189,14 @@ class ChengAnalysis:
         self.rgb6 = (K.pack_up3k3_x6(w1, wsk) if x6 and w1.shape[1] == 3 and w1.shape[0] % 16 == 0
                      and tuple(wsk.shape[1:]) == (3, 1, 1) else None)
 
-    def forward(self, x4, save=False):
+    def forward(self, x4, save=False, inputs=None):
+        """inputs: an optional list that receives every block's input and the last conv's (the weight gradients of
+        the fine-tune, train_cheng)."""
         h, saved = x4, []
         for i, blk in enumerate(self.blocks):
             t = f"{self.tag}.{i}"
+            if inputs is not None:
+                inputs.append(h)
             if blk[0] == "rbs":
                 _, c1, c2, sk, gd = blk
                 a1 = c1.forward(h, K.EPI_LRELU, tag=f"{t}.conv1.fwd")
@@ -210,6 +214,8 @@ class ChengAnalysis:
                 a2 = torch.empty_like(a1) if save else None
                 h = c2.forward(a1, K.EPI_LRELU, res=h, save_x=a2, tag=f"{t}.conv2.fwd")
                 saved.append((a1, a2) if save else None)
+        if inputs is not None:
+            inputs.append(h)
         y = self.last.forward(h, K.EPI_BIAS, tag=f"{self.tag}.6.fwd")
         return y, saved
 
@@ -264,10 +270,13 @@ class ChengSynthesis:
                                     _gdn(sd, f"{pre}.igdn")))
         self.last = Subpel(sd[_k(prefix, "7.0.weight")], sd[_k(prefix, "7.0.bias")], x6=x6)
 
-    def forward(self, y4, save=False):
+    def forward(self, y4, save=False, inputs=None):
+        """inputs: as ChengAnalysis.forward."""
         h, saved = y4, []
         for i, blk in enumerate(self.blocks):
             t = f"{self.tag}.{i}"
+            if inputs is not None:
+                inputs.append(h)
             if blk[0] == "rb":
                 _, c1, c2 = blk
                 a1 = c1.forward(h, K.EPI_LRELU, tag=f"{t}.conv1.fwd")
@@ -283,6 +292,8 @@ class ChengSynthesis:
                 h = cv.forward(a1, K.EPI_IGDN, gdn=gd, res=r, save_x=yg, save_s=s, tag=f"{t}.conv.fwd")
                 del r
                 saved.append((a1, yg, s) if save else None)
+        if inputs is not None:
+            inputs.append(h)
         xh = self.last.forward(h, K.EPI_BIAS, tag=f"{self.tag}.7.fwd")
         return xh, saved
 

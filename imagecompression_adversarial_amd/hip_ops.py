@@ -685,6 +685,20 @@ def abs_bwd_(g4, x4):
     return g4
 
 
+def lrelu_bwd(g4, a4):
+    """g * lrelu'(a) into a new tensor (a: the saved leaky-ReLU output)."""
+    out = torch.empty_like(g4)
+    call("ica_lrelu_bwd", ptr(g4), ptr(a4), ptr(out), g4.numel(), stream())
+    return out
+
+
+def gdn_t(g4, y4, s4, inverse):
+    """t = dL/dn of a GDN / IGDN layer from g = dL/dy and its saved (y, s) (ica_gdn_t)."""
+    out = torch.empty_like(g4)
+    call("ica_gdn_t", ptr(g4), ptr(y4), ptr(s4), ptr(out), g4.numel(), int(bool(inverse)), stream())
+    return out
+
+
 def gdn_xsq(y4, s4):
     out = torch.empty_like(y4)
     call("ica_gdn_xsq", ptr(y4), ptr(s4), ptr(out), y4.numel(), stream())

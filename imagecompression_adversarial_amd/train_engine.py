@@ -1,4 +1,5 @@
-"""Train-mode forward + RateDistortionLoss + backward of the bmshj2018 codecs on the HIP kernels.
+"""Train-mode forward + RateDistortionLoss + backward of the bmshj2018 codecs on the HIP kernels (cheng2020-anchor:
+train_cheng.ChengTrainStep, dispatched from RDTrainer.step).
 
 This is the inner piece of the adversarial fine-tune:
 
@@ -112,6 +113,9 @@ class RDTrainer:
             raise ValueError(f"metric {metric!r}: the HIP trainer supports mse and ms-ssim (lpips is out of scope)")
         self.net, self.metric, self.lmbda = net, metric, float(lmbda)
         self.kind = net.model_kind
+        if self.kind not in ("factorized", "hyper", "cheng2020"):
+            raise NotImplementedError(f"the HIP trainer covers bmshj2018 and cheng2020-anchor, not {self.kind!r}")
+        self._cheng = None
         # train.py:77-83: lambda == 100 is the reference's "Inf mode", the rate term leaves the loss (lamb_r = 0)
         self.lamb_r = 0.0 if self.lmbda == 100 else 1.0
         if self.lamb_r == 0.0:
@@ -154,11 +158,35 @@ class RDTrainer:
         K.eb_param_scatter(gprm, [self.params[n].detach() for n in names], [self._g(n) for n in names], C)
         return gv
 
+    def _loss(self, xh4, x, liks, bscale):
+        """RateDistortionLoss (train.py:52-96, training=True: no clamp on x_hat): (loss, bpp, distortion, dL/dx_hat
+        as nChw4c)."""
+        B, _, H, W = x.shape
+        bpp = sum(torch.log(l.clamp_min(1.0 / 65536)).sum() for l in liks) * bscale
+        g4 = torch.zeros_like(xh4)
+        if self.metric == "mse":
+            dist = K.sqdiff_mean(K.from_nc4(xh4, 3), x).mean()
+            K.mse_grad_(xh4, x, g4, self.lmbda * 255.0 ** 2 * 2.0 / (B * 3 * H * W))
+            loss = self.lmbda * 255.0 ** 2 * dist + self.lamb_r * bpp
+        else:
+            xh = K.from_nc4(xh4, 3)
+            v, gX, _ = MS.ms_ssim_value_and_grad(xh, x, torch.full((B,), -self.lmbda / B, device=x.device),
+                                                 data_range=1.0, mode=0)
+            dist = v.mean()
+            g4 = K.to_nc4(gX)
+            loss = self.lmbda * (1.0 - dist) + self.lamb_r * bpp
+        return loss, bpp, dist, g4
+
     # ------------------------------------------------------------------ #
     def step(self, x: torch.Tensor, noise_y: torch.Tensor | None = None, noise_z: torch.Tensor | None = None):
         """One train-mode forward + loss + backward.  x: [B,3,H,W] on the device (H, W multiples of 64).
         noise_y / noise_z: optional NCHW U(-1/2,1/2) quantisation noise (drawn here when None).
         Returns {"loss", "bpp_loss", "distortion_loss"} as 0-d device tensors; grads in p.grad."""
+        if self.kind == "cheng2020":
+            if self._cheng is None:
+                from .train_cheng import ChengTrainStep
+                self._cheng = ChengTrainStep(self)
+            return self._cheng.step(x, noise_y, noise_z)
         x = x.contiguous()
         B, _, H, W = x.shape
         ck = self.net.kernels()
@@ -193,21 +221,7 @@ class RDTrainer:
             yt4, ylik4, _ = K.gc_likelihood(y4, M, sig4, None, True, ny4)
             liks = [ylik4, zlik4]
         xh4, ss = ck.gs.forward(yt4, save=True, split=False)
-
-        # ---- loss (train.py:52-96, training=True: no clamp on x_hat) ----
-        bpp = sum(torch.log(l.clamp_min(1.0 / 65536)).sum() for l in liks) * bscale
-        g4 = torch.zeros_like(xh4)
-        if self.metric == "mse":
-            dist = K.sqdiff_mean(K.from_nc4(xh4, 3), x).mean()
-            K.mse_grad_(xh4, x, g4, self.lmbda * 255.0 ** 2 * 2.0 / (B * 3 * H * W))
-            loss = self.lmbda * 255.0 ** 2 * dist + self.lamb_r * bpp
-        else:
-            xh = K.from_nc4(xh4, 3)
-            v, gX, _ = MS.ms_ssim_value_and_grad(xh, x, torch.full((B,), -self.lmbda / B, device=x.device),
-                                                 data_range=1.0, mode=0)
-            dist = v.mean()
-            g4 = K.to_nc4(gX)
-            loss = self.lmbda * (1.0 - dist) + self.lamb_r * bpp
+        loss, bpp, dist, g4 = self._loss(xh4, x, liks, bscale)
 
         # ---- backward ----
         gyt = self._g_s_backward(ck.gs, g4, yt4, ss)

@@ -346,7 +346,7 @@ int ica_wgrad_nsplit(int A, int Bc, long nchunks);
 /* out[a][b][ky][kx] (+)= sum_{n,p} Sm[n][a][p] * Lg[n][b][S*p + k - P]   (nChw4c operands)
  *   conv   W[o][c]:  Sm = dL/dy (a = o, small grid = output), Lg = x (b = c, big grid = input)
  *   deconv W[c][o]:  Sm = x (a = c, small grid = input),      Lg = dL/dy (b = o, big grid = output)
- * KS,S in {(5,2),(3,1),(1,1)}; deterministic (fixed-order split reduction). */
+ * KS,S in {(5,2),(3,1),(1,1),(3,2),(1,2),(5,1)}; deterministic (fixed-order split reduction). */
 int ica_wgrad(const float* Sm, const float* Lg, float* ws, float* out, int N, int A, int Bc, int Hs, int Ws, int Hb,
               int Wb, int KS, int S, int P, int nsplit, int accumulate, hipStream_t stream);
 /* out[c] (+)= sum over n, pixels of x (nChw4c): bias and GDN beta' gradients. */
@@ -354,6 +354,13 @@ int ica_channel_sum(const float* x, float* out, int N, int C, int H, int W, int 
 int ica_relu_bwd(float* g, const float* y, long n, hipStream_t stream);          /* g *= (y > 0) */
 int ica_abs_bwd(float* g, const float* x, long n, hipStream_t stream);           /* g *= sign(x) */
 int ica_gdn_xsq(const float* y, const float* s, float* out, long n, hipStream_t stream); /* (y/s)^2 */
+/* out = g * lrelu'(a) (a: the layer's saved leaky-ReLU output, slope 0.01): the pre-activation gradient of the
+ * cheng2020 / mbt2018 leaky-ReLU layers (train.py:358-359 through CompressAI's nn.LeakyReLU). */
+int ica_lrelu_bwd(const float* g, const float* a, float* out, long n, hipStream_t stream);
+/* t = dL/dn of a GDN (inverse 0: t = -0.5 g y s^2) or IGDN (inverse 1: t = 0.5 g y / s^2) layer from g = dL/dy and
+ * its saved (y, s) (utils/ops.py GDN; the GDN parameter gradients of the k3 residual layers, whose backward launch
+ * fuses the GDN backward without writing t). */
+int ica_gdn_t(const float* g, const float* y, const float* s, float* t, long n, int inverse, hipStream_t stream);
 /* NonNegativeParametrizer backward (utils/ops.py:58-81): gout (+)= g' * 2 max(p,bound), LowerBound gate. */
 int ica_reparam_bwd(const float* p, const float* gprime, float* gout, long n, float bound, int accumulate,
                     hipStream_t stream);

@@ -54,7 +54,7 @@ def _ssim_pc(X, Y, win, data_range=1.0, K=(0.01, 0.03)):
 def ms_ssim_per_image(X, Y, data_range=1.0, win_size=11, win_sigma=1.5):
     """pytorch_msssim.ms_ssim(..., size_average=False) -> [N] (mean over channels)."""
     assert min(X.shape[-2:]) > (win_size - 1) * 2 ** 4, "image too small for 5-level MS-SSIM"
-    win = gauss_1d(win_size, win_sigma)
+    win = gauss_1d(win_size, win_sigma).to(X.dtype)   # float64 replays (fp32: unchanged)
     w = torch.tensor(MS_WEIGHTS, dtype=X.dtype)
     mcs = []
     for i in range(len(MS_WEIGHTS)):
