@@ -828,6 +828,18 @@ def _ar_decompress(model, strings, shape):
         return {"x_hat": K.from_nc4(xh4, 3).clamp_(0, 1)}
 
 
+def _train_values(model, x, train_forward):
+    """The train-mode forward's values (random quantisation noise) of a joint-prior model; a call that would need
+    gradients is refused (no silent gradient hole, as _ForwardOnly): train through train_engine.RDTrainer."""
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in model.parameters())):
+        raise NotImplementedError(f"{type(model).__name__} is forward-only on the module API; freeze it "
+                                  "(requires_grad_(False)) or train with train_engine.RDTrainer")
+    sd = {k: v.detach() for k, v in model.state_dict().items()}
+    f = train_forward(model.kernels("fp32"), sd.__getitem__, K.to_nc4(x.detach().contiguous()))
+    return {"x_hat": K.from_nc4(f["xh4"], 3),
+            "likelihoods": {"y": K.from_nc4(f["ylik4"], model.M), "z": K.from_nc4(f["zlik4"], model.N)}}
+
+
 class Cheng2020Anchor(CompressionModel):
     """compressai.models.Cheng2020Anchor (JointAutoregressiveHierarchicalPriors with residual transforms).
     Eval-mode forward (the attack path) and the train-mode forward's values; the fine-tune's gradients come from
@@ -849,15 +861,8 @@ class Cheng2020Anchor(CompressionModel):
 
     def forward(self, x):
         if self.training:
-            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
-                # no silent gradient hole (as _ForwardOnly): train through train_engine.RDTrainer
-                raise NotImplementedError("Cheng2020Anchor is forward-only on the module API; freeze it "
-                                          "(requires_grad_(False)) or train with train_engine.RDTrainer")
             from .train_cheng import train_forward
-            sd = {k: v.detach() for k, v in self.state_dict().items()}
-            f = train_forward(self.kernels("fp32"), sd.__getitem__, K.to_nc4(x.detach().contiguous()))
-            return {"x_hat": K.from_nc4(f["xh4"], 3),
-                    "likelihoods": {"y": K.from_nc4(f["ylik4"], self.M), "z": K.from_nc4(f["zlik4"], self.N)}}
+            return _train_values(self, x, train_forward)
         res = self.kernels().forward(K.to_nc4(x.detach().contiguous()))
         return {"x_hat": K.from_nc4(res["x_hat4"], 3),
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}
@@ -927,7 +932,8 @@ class AeOneLayer(CompressionModel):
 
 class JointAutoregressiveHierarchicalPriors(CompressionModel):
     """compressai.models.JointAutoregressiveHierarchicalPriors (mbt2018): bmshj2018 g_a / g_s, LReLU hyper
-    transforms, masked 5x5 context model.  Eval-mode forward (the attack path, anchors/model.py:95-104)."""
+    transforms, masked 5x5 context model.  Eval-mode forward (the attack path, anchors/model.py:95-104) and the
+    train-mode forward's values; the fine-tune's gradients come from train_engine.RDTrainer -> train_mbt."""
     model_kind = "context"
 
     def __init__(self, N=192, M=192, **kwargs):
@@ -944,7 +950,8 @@ class JointAutoregressiveHierarchicalPriors(CompressionModel):
 
     def forward(self, x):
         if self.training:
-            raise NotImplementedError("mbt2018 training is out of scope on the HIP path (eval forward only)")
+            from .train_mbt import train_forward
+            return _train_values(self, x, train_forward)
         res = self.kernels().forward(K.to_nc4(x.detach().contiguous()))
         return {"x_hat": K.from_nc4(res["x_hat4"], 3),
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}

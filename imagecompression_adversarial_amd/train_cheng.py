@@ -43,6 +43,28 @@ def _conv(P, pre, stride=1, mask=None):
     return Conv3(P(f"{pre}.weight"), P(f"{pre}.bias"), stride, mask=mask)
 
 
+def entropy_forward(P, y4, M, params4, noise_y=None):
+    """The joint entropy model in train mode (cheng2020 and mbt2018, anchors/model.py:97-106): y_hat = y + u, the
+    masked context model, entropy_parameters(cat(h_s params, ctx)) -> (scales, means), GaussianConditional."""
+    B = y4.shape[0]
+    if noise_y is None:
+        noise_y = torch.empty((B, M, y4.shape[2], y4.shape[3]), device=y4.device).uniform_(-0.5, 0.5)
+    ny4 = K.to_nc4(noise_y.contiguous())
+    yh4 = y4 + ny4                                     # y_hat = quantize(y, "noise") (train mode)
+    ctxc = _conv(P, "context_prediction", mask=context_mask(5))
+    ctx4 = ctxc.forward(yh4, K.EPI_BIAS)
+    ep = [_conv(P, f"entropy_parameters.{i}") for i in (0, 2, 4)]
+    t0 = torch.cat((params4, ctx4), dim=1)
+    e0 = ep[0].forward(t0, K.EPI_LRELU)
+    e1 = ep[1].forward(e0, K.EPI_LRELU)
+    gp4 = ep[2].forward(e1, K.EPI_BIAS)
+    c4 = (M + 3) // 4
+    scales4, means4 = gp4[:, :c4].contiguous(), gp4[:, c4:].contiguous()
+    yt4, ylik4, _ = K.gc_likelihood(y4, M, scales4, means4, True, ny4)
+    return {"yh4": yh4, "ctxc": ctxc, "ep": ep, "t0": t0, "e0": e0, "e1": e1, "scales4": scales4,
+            "means4": means4, "yt4": yt4, "ylik4": ylik4}
+
+
 def train_forward(ck, P, x4, noise_y=None, noise_z=None):
     """The train-mode forward of cheng2020 (oracle/codec.cheng_forward, training=True) with every activation the
     backward reads.  ck: the model's fp32 ChengKernels; P(name): the detached parameter; noise_y / noise_z: NCHW
@@ -67,23 +89,13 @@ def train_forward(ck, P, x4, noise_y=None, noise_z=None):
     s2 = hs4.forward(s1, K.EPI_LRELU)
     s3 = hs6.forward(s2, K.EPI_LRELU)
     params4 = hs8.forward(s3, K.EPI_BIAS)
-    if noise_y is None:
-        noise_y = torch.empty((B, N, y4.shape[2], y4.shape[3]), device=x4.device).uniform_(-0.5, 0.5)
-    ny4 = K.to_nc4(noise_y.contiguous())
-    yh4 = y4 + ny4                                     # y_hat = quantize(y, "noise") (train mode)
-    ctxc = _conv(P, "context_prediction", mask=context_mask(5))
-    ctx4 = ctxc.forward(yh4, K.EPI_BIAS)
-    ep = [_conv(P, f"entropy_parameters.{i}") for i in (0, 2, 4)]
-    t0 = torch.cat((params4, ctx4), dim=1)
-    e0 = ep[0].forward(t0, K.EPI_LRELU)
-    e1 = ep[1].forward(e0, K.EPI_LRELU)
-    gp4 = ep[2].forward(e1, K.EPI_BIAS)
-    c4 = (N + 3) // 4
-    scales4, means4 = gp4[:, :c4].contiguous(), gp4[:, c4:].contiguous()
-    yt4, ylik4, _ = K.gc_likelihood(y4, N, scales4, means4, True, ny4)
+    ent = entropy_forward(P, y4, N, params4, noise_y)
+    yh4 = ent["yh4"]
     in_s = []
     xh4, ss = ck.gs.forward(yh4, save=True, inputs=in_s)
-    return {k: v for k, v in locals().items() if k not in ("ck", "P", "B", "N")}
+    out = {k: v for k, v in locals().items() if k not in ("ck", "P", "B", "N", "ent")}
+    out.update(ent)
+    return out
 
 
 class ChengTrainStep:
@@ -134,6 +146,25 @@ class ChengTrainStep:
         t = K.gdn_t(g_sum, yg, s, inverse)
         gdn_param_grads(self._p(f"{pre}.beta"), self._p(f"{pre}.gamma"), t, (yg, s), C, self._g(f"{pre}.beta"),
                         self._g(f"{pre}.gamma"))
+
+    def context_backward(self, gy, ylik4, gscale, yt4, means4, scales4, M, ep, t0, e0, e1, params4, yh4, ctxc):
+        """GaussianConditional (scales, means) -> entropy_parameters (1x1, leaky ReLU) -> the masked context model:
+        weight gradients; dL/dy (GC) and dL/d(y_hat) (context) added into gy; returns dL/d(h_s output)."""
+        gl_y = K.bpp_grad(ylik4, gscale)
+        gv, gsig = K.gc_bwd(yt4 - means4, scales4, gl_y, M)
+        gy.add_(gv)                                         # y_tilde = y + u: dL/dy += dL/dv
+        ggp = torch.cat((gsig, -gv), dim=1)                 # d/d(means) = -d/dv
+        self._wb(ggp, 2 * M, e1, ep[2].Cin, 1, 1, "entropy_parameters.4")
+        g = K.lrelu_bwd(ep[2].dgrad(ggp), e1)
+        self._wb(g, ep[1].Cout, e0, ep[1].Cin, 1, 1, "entropy_parameters.2")
+        g = K.lrelu_bwd(ep[1].dgrad(g), e0)
+        self._wb(g, ep[0].Cout, t0, ep[0].Cin, 1, 1, "entropy_parameters.0")
+        g = ep[0].dgrad(g)
+        cp = params4.shape[1]
+        gparams, gctx = g[:, :cp].contiguous(), g[:, cp:].contiguous()
+        self._wb(gctx, 2 * M, yh4, M, 5, 1, "context_prediction", mask=context_mask(5))
+        gy.add_(ctxc.dgrad(gctx))
+        return gparams
 
     # ------------------------------------------------------------------ transforms
     def g_a_backward(self, ga, gy4, saved, inputs):
@@ -231,20 +262,7 @@ class ChengTrainStep:
         # ---- backward ----
         gy = self.g_s_backward(ck.gs, g4, ss, in_s)        # dL/d(y_hat) from g_s
         del ss, in_s, g4
-        gl_y = K.bpp_grad(ylik4, gscale)
-        gv, gsig = K.gc_bwd(yt4 - means4, scales4, gl_y, N)
-        gy.add_(gv)                                         # y_tilde = y + u: dL/dy += dL/dv
-        ggp = torch.cat((gsig, -gv), dim=1)                 # d/d(means) = -d/dv
-        self._wb(ggp, 2 * N, e1, ep[2].Cin, 1, 1, "entropy_parameters.4")
-        g = K.lrelu_bwd(ep[2].dgrad(ggp), e1)
-        self._wb(g, ep[1].Cout, e0, ep[1].Cin, 1, 1, "entropy_parameters.2")
-        g = K.lrelu_bwd(ep[1].dgrad(g), e0)
-        self._wb(g, ep[0].Cout, t0, ep[0].Cin, 1, 1, "entropy_parameters.0")
-        g = ep[0].dgrad(g)
-        cp = params4.shape[1]
-        gparams, gctx = g[:, :cp].contiguous(), g[:, cp:].contiguous()
-        self._wb(gctx, 2 * N, yh4, N, 5, 1, "context_prediction", mask=context_mask(5))
-        gy.add_(ctxc.dgrad(gctx))
+        gparams = self.context_backward(gy, ylik4, gscale, yt4, means4, scales4, N, ep, t0, e0, e1, params4, yh4, ctxc)
         # h_s backward
         self._wb(gparams, hs8.Cout, s3, hs8.Cin, 3, 1, "h_s.8")
         g = hs8.dgrad(gparams, K.EPI_LRELU_BWD, saved=(s3, None))

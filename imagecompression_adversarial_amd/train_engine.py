@@ -1,5 +1,5 @@
 """Train-mode forward + RateDistortionLoss + backward of the bmshj2018 codecs on the HIP kernels (cheng2020-anchor:
-train_cheng.ChengTrainStep, dispatched from RDTrainer.step).
+train_cheng.ChengTrainStep; mbt2018: train_mbt.MbtTrainStep; both dispatched from RDTrainer.step).
 
 This is the inner piece of the adversarial fine-tune:
 
@@ -113,9 +113,10 @@ class RDTrainer:
             raise ValueError(f"metric {metric!r}: the HIP trainer supports mse and ms-ssim (lpips is out of scope)")
         self.net, self.metric, self.lmbda = net, metric, float(lmbda)
         self.kind = net.model_kind
-        if self.kind not in ("factorized", "hyper", "cheng2020"):
-            raise NotImplementedError(f"the HIP trainer covers bmshj2018 and cheng2020-anchor, not {self.kind!r}")
-        self._cheng = None
+        if self.kind not in ("factorized", "hyper", "cheng2020", "context"):
+            raise NotImplementedError(f"the HIP trainer covers bmshj2018, mbt2018 and cheng2020-anchor, not "
+                                      f"{self.kind!r}")
+        self._joint = None   # cheng2020 / mbt2018 (train_cheng, train_mbt)
         # train.py:77-83: lambda == 100 is the reference's "Inf mode", the rate term leaves the loss (lamb_r = 0)
         self.lamb_r = 0.0 if self.lmbda == 100 else 1.0
         if self.lamb_r == 0.0:
@@ -182,11 +183,14 @@ class RDTrainer:
         """One train-mode forward + loss + backward.  x: [B,3,H,W] on the device (H, W multiples of 64).
         noise_y / noise_z: optional NCHW U(-1/2,1/2) quantisation noise (drawn here when None).
         Returns {"loss", "bpp_loss", "distortion_loss"} as 0-d device tensors; grads in p.grad."""
-        if self.kind == "cheng2020":
-            if self._cheng is None:
-                from .train_cheng import ChengTrainStep
-                self._cheng = ChengTrainStep(self)
-            return self._cheng.step(x, noise_y, noise_z)
+        if self.kind in ("cheng2020", "context"):
+            if self._joint is None:
+                if self.kind == "cheng2020":
+                    from .train_cheng import ChengTrainStep as Step
+                else:
+                    from .train_mbt import MbtTrainStep as Step
+                self._joint = Step(self)
+            return self._joint.step(x, noise_y, noise_z)
         x = x.contiguous()
         B, _, H, W = x.shape
         ck = self.net.kernels()

@@ -1,9 +1,9 @@
-"""GPU parity of the cheng2020-anchor adversarial fine-tune (SURVEY §8 a15 for ``-m cheng2020``; reference
-train.py:249-366 fine-tunes whatever coder.load_model builds) against the oracle's autograd of its restated
-cheng2020 forward (oracle/codec.cheng_forward, training=True): the gradient of every main parameter with fixed
-quantisation noise, and one whole outer step (inner attack, RD backward, clip, Adam, aux Adam) against
-oracle.attack.adv_train_step.  The cheng2020 architecture is restated from public CompressAI: parity unpinned
-beyond its primitives (oracle/codec.py header)."""
+"""GPU parity of the adversarial fine-tune of the joint-prior codecs (SURVEY §8 a15 for ``-m cheng2020`` and
+``-m context`` = mbt2018; reference train.py:249-366 fine-tunes whatever coder.load_model builds) against the
+oracle's autograd of its restated forwards (oracle/codec.cheng_forward / mbt_forward, training=True): the gradient of
+every main parameter with fixed quantisation noise, and one whole outer step (inner attack, RD backward, clip, Adam,
+aux Adam) against oracle.attack.adv_train_step.  Both architectures are restated from public CompressAI: parity
+unpinned beyond their primitives (oracle/codec.py header)."""
 import pytest
 import torch
 
@@ -20,20 +20,23 @@ def rnd(shape, seed, lo=0.0, hi=1.0):
     return torch.rand(shape, generator=g) * (hi - lo) + lo
 
 
-def _net(P, q):
+def _net(P, q, model="cheng2020"):
     from imagecompression_adversarial_amd import codec
-    net = codec.cheng2020_anchor(q)
+    net = codec.cheng2020_anchor(q) if model == "cheng2020" else codec.mbt2018(q)
     sd = net.state_dict()
     sd.update({k: v.reshape(sd[k].shape) for k, v in P.items() if k in sd})
     net.load_state_dict(sd)
     return net.to(DEV).train()
 
 
-def _path_masks(f):
-    """The side of zero of every leaky-ReLU output of the HIP train forward (train_cheng.train_forward's dict), NCHW
-    bool on the CPU, in the order oracle/codec.cheng_forward calls lrelu: g_a (per block conv1 [, conv2]), h_a (4),
-    h_s (4), entropy_parameters (2), g_s (per block conv1 [, conv2] / subpel)."""
+def _path_masks(f, model="cheng2020"):
+    """The side of zero of every leaky-ReLU output of the HIP train forward (train_cheng / train_mbt .train_forward's
+    dict), NCHW bool on the CPU, in the order the oracle forward calls lrelu.  cheng2020: g_a (per block conv1
+    [, conv2]), h_a (4), h_s (4), entropy_parameters (2), g_s (per block conv1 [, conv2] / subpel); mbt2018: h_a (2),
+    h_s (2), entropy_parameters (2)."""
     from imagecompression_adversarial_amd import hip_ops as K
+    if model == "context":
+        return [(K.from_nc4(f[k], f[k].shape[1] * 4) > 0).cpu() for k in ("z0", "z1", "s0", "s1", "e0", "e1")]
     acts = []
     for blk in f["sa"]:
         acts += list(blk[:2]) if len(blk) == 2 else [blk[0]]
@@ -43,7 +46,7 @@ def _path_masks(f):
     return [(K.from_nc4(t, t.shape[1] * 4) > 0).cpu() for t in acts]
 
 
-def _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch):
+def _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch, model="cheng2020"):
     """Loss values and parameter gradients of the float64 oracle train forward whose every leaky ReLU takes the HIP
     path's side of zero (masks, cheng_forward call order).  Asserts that every sign disagreement is a kink: a float64
     pre-activation within KINK_REL of its tensor's max of zero.  Returns (loss dict, grads, largest disagreement)."""
@@ -63,7 +66,7 @@ def _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch):
 
     P64 = {k: v.double().requires_grad_(True) for k, v in P.items()}
     monkeypatch.setattr(oc, "lrelu", lrelu_path)
-    res = oc.forward(P64, x.double(), "cheng2020", training=True, noise_y=ny.double(), noise_z=nz.double())
+    res = oc.forward(P64, x.double(), model, training=True, noise_y=ny.double(), noise_z=nz.double())
     assert not queue, len(queue)
     out = oa.rd_loss(res, x.double(), metric, lmbda)
     out["loss"].backward()
@@ -71,34 +74,40 @@ def _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch):
     return out, {k: v.grad for k, v in P64.items() if v.grad is not None}, worst[0]
 
 
-@pytest.mark.parametrize("q,metric,H,W", [(6, "mse", 128, 128), (6, "ms-ssim", 192, 192), (2, "mse", 128, 192)])
-def test_cheng_rd_backward_vs_float64(q, metric, H, W, monkeypatch):
-    """Train-mode forward + RateDistortionLoss + backward (train_cheng.ChengTrainStep) against the float64 oracle
-    (oracle/codec.cheng_forward, training=True) evaluated with the HIP forward's own leaky-ReLU sides: every sign
+@pytest.mark.parametrize("model,q,metric,H,W", [
+    ("cheng2020", 6, "mse", 128, 128), ("cheng2020", 6, "ms-ssim", 192, 192), ("cheng2020", 2, "mse", 128, 192),
+    ("context", 3, "mse", 128, 128), ("context", 6, "ms-ssim", 192, 192)])
+def test_joint_rd_backward_vs_float64(model, q, metric, H, W, monkeypatch):
+    """Train-mode forward + RateDistortionLoss + backward (train_cheng.ChengTrainStep / train_mbt.MbtTrainStep; mbt2018
+    q6 has M = 320) against the float64 oracle (oracle/codec.cheng_forward / mbt_forward, training=True) evaluated
+    with the HIP forward's own leaky-ReLU sides: every sign
     disagreement is a kink (< KINK_REL of the tensor max), loss values at 1e-5, every main parameter's gradient within
     2e-4 of its max.  (Against the plain fp32 oracle the leaky-ReLU layers' weight gradients differ by up to
     ~4e-3 of max at these shapes: each fp32 evaluation puts a few kink pre-activations on its own side, and the
     fp32 oracle itself is 1.2e-3 off float64 on g_s.4.conv1 at q2.)"""
     from imagecompression_adversarial_amd import hip_ops as K
     from imagecompression_adversarial_amd.train import LAMBS
-    from imagecompression_adversarial_amd.train_cheng import train_forward
     from imagecompression_adversarial_amd.train_engine import RDTrainer
-    P = oc.perturb_params(oc.init_params("cheng2020", q, seed=0), seed=1)
-    N, _ = oc.model_channels("cheng2020", q)
+    if model == "cheng2020":
+        from imagecompression_adversarial_amd.train_cheng import train_forward
+    else:
+        from imagecompression_adversarial_amd.train_mbt import train_forward
+    P = oc.perturb_params(oc.init_params(model, q, seed=0), seed=1)
+    N, M = oc.model_channels(model, q)
     B = 2
     x = rnd((B, 3, H, W), 5)
-    ny = rnd((B, N, H // 16, W // 16), 6, -0.5, 0.5)
+    ny = rnd((B, M, H // 16, W // 16), 6, -0.5, 0.5)
     nz = rnd((B, N, H // 64, W // 64), 7, -0.5, 0.5)
     lmbda = LAMBS[metric][q - 1]
-    net = _net(P, q)
+    net = _net(P, q, model)
     tr = RDTrainer(net, metric, lmbda)
     got = tr.step(x.to(DEV), ny.to(DEV), nz.to(DEV))
     named = dict(net.named_parameters())
     f = train_forward(net.kernels("fp32"), lambda k: named[k].detach(), K.to_nc4(x.to(DEV)), ny.to(DEV), nz.to(DEV))
-    masks = _path_masks(f)
+    masks = _path_masks(f, model)
     del f
     torch.cuda.synchronize()
-    ref, grads, dis = _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch)
+    ref, grads, dis = _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch, model)
     for k in ("loss", "bpp_loss", "distortion_loss"):
         assert abs(float(got[k]) - float(ref[k])) <= 1e-5 * max(abs(float(ref[k])), 1.0), k
     worst, checked = [], 0
@@ -115,12 +124,13 @@ def test_cheng_rd_backward_vs_float64(q, metric, H, W, monkeypatch):
     assert worst[0][0] < 2e-4, worst[:5]
 
 
-def test_cheng_train_forward_values():
+@pytest.mark.parametrize("model", ["cheng2020", "context"])
+def test_joint_train_forward_values(model):
     """The module API's train-mode forward: refused while parameters require grad (no silent gradient hole: train
     through RDTrainer), values with frozen parameters (its own random quantisation noise): likelihoods in (0, 1],
     a finite x_hat of the input's shape."""
-    P = oc.perturb_params(oc.init_params("cheng2020", 6, seed=0), seed=1)
-    net = _net(P, 6)
+    P = oc.perturb_params(oc.init_params(model, 6, seed=0), seed=1)
+    net = _net(P, 6, model)
     x = rnd((1, 3, 64, 64), 8).to(DEV)
     with pytest.raises(NotImplementedError):
         net(x)
@@ -133,25 +143,26 @@ def test_cheng_train_forward_values():
     assert torch.isfinite(out["x_hat"]).all() and out["x_hat"].shape == x.shape
 
 
-def test_cheng_adv_train_step_vs_oracle():
-    """One whole outer step of train.py --adv for cheng2020 q6 (x6 inner attack, 4 inner steps, the cheng attack
-    tests' input) vs oracle.attack.adv_train_step: branch sequence step by step; the adversarial batch at the cheng2020
-    attack tolerance (2e-3 of max, leaky-ReLU kinks: tests/test_gpu_cheng.py); loss values at 1e-4; the first Adam
-    step's parameter moves with 99.9 % within 1e-2 of the step size and every one within 2 steps (sign flips of
-    near-zero gradients)."""
+@pytest.mark.parametrize("model", ["cheng2020", "context"])
+def test_joint_adv_train_step_vs_oracle(model):
+    """One whole outer step of train.py --adv for cheng2020 / mbt2018 q6 (x6 inner attack, 4 inner steps, the cheng
+    attack tests' input) vs oracle.attack.adv_train_step: branch sequence step by step; the adversarial batch at the
+    cheng2020 attack tolerance (2e-3 of max, leaky-ReLU kinks: tests/test_gpu_cheng.py); loss values at 1e-4; the
+    first Adam step's parameter moves with 99.9 % within 1e-2 of the step size and every one within 2 steps (sign
+    flips of near-zero gradients)."""
     from types import SimpleNamespace
     from imagecompression_adversarial_amd import coder
     from imagecompression_adversarial_amd.train import LAMBS, adv_step
     from imagecompression_adversarial_amd.train_engine import RDTrainer
     q, steps, B, H, W = 6, 4, 2, 64, 64
-    P = oc.perturb_params(oc.init_params("cheng2020", q, seed=0), seed=1)
-    N, _ = oc.model_channels("cheng2020", q)
+    P = oc.perturb_params(oc.init_params(model, q, seed=0), seed=1)
+    N, M = oc.model_channels(model, q)
     x = rnd((B, 3, H, W), 34)
-    ny = rnd((B, N, H // 16, W // 16), 42, -0.5, 0.5)
+    ny = rnd((B, M, H // 16, W // 16), 42, -0.5, 0.5)
     nz = rnd((B, N, H // 64, W // 64), 43, -0.5, 0.5)
     lr_train, metric = 1e-4, "mse"
     lmbda = LAMBS[metric][q - 1]
-    net = _net(P, q)
+    net = _net(P, q, model)
     opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=lr_train))
     tr = RDTrainer(net, metric, lmbda)
     args = SimpleNamespace(steps=steps, epsilon=16.0, noise=1e-4, lr_attack=0.01, att_metric="L2", clamp=True,
@@ -160,7 +171,7 @@ def test_cheng_adv_train_step_vs_oracle():
     out, batch_adv = adv_step(net, tr, opt, aux, x.to(DEV), args, qnoise=(ny.to(DEV), nz.to(DEV)), record=br)
     torch.cuda.synchronize()
     rec = []
-    Pn, ref_out, ref_aux, ref_adv = oa.adv_train_step(P, x, steps=steps, model="cheng2020", metric=metric,
+    Pn, ref_out, ref_aux, ref_adv = oa.adv_train_step(P, x, steps=steps, model=model, metric=metric,
                                                        lmbda=lmbda, lr_train=lr_train, noise_y=ny, noise_z=nz,
                                                        record=rec)
     assert len(br) == len(rec) == steps
