@@ -479,8 +479,10 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
     // before its own split.  Same MFMA order as the single-buffer loop (bit-identical results).
     static_assert(KK % 3 == 0, "x6 conv_down ring: KK a multiple of 3");
     constexpr bool MK = (FX & FX_MASK) != 0, US = (FX & FX_UNSHUF) != 0;
-    constexpr int NF = (NE * PLANE + 255) / 256, PUTD = 3;
-    static_assert(NF + PUTD <= KK, "x6 conv_down: the chunk's fill must land inside its taps");
+    // FPT quads per thread issued per tap (1 for the stride-1 patches; 2 for the stride-2 forward's 2.5x larger
+    // patch, NF = 9-10), each split PUTD taps after its load
+    constexpr int NF = (NE * PLANE + 255) / 256, PUTD = 3, FPT = (NF + KK - PUTD - 1) / (KK - PUTD);
+    static_assert((NF + FPT - 1) / FPT + PUTD <= KK, "x6 conv_down: the chunk's fill must land inside its taps");
     const unsigned xplane = (unsigned)p.Hin * p.Win;
     const __amdgpu_buffer_rsrc_t xr =
         uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * xplane * 16, Cin4 * xplane * 16u);
@@ -564,8 +566,10 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
 #pragma unroll
         for (int tap = 0; tap < KK; ++tap) {
           ldw(fr[(R0 + tap + 1) & 1], ch * KK + tap + 1);
-          if (tap < NF) fload(ch + 1, tap);
-          if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
+#pragma unroll
+          for (int i = tap * FPT; i < (tap + 1) * FPT && i < NF; ++i) fload(ch + 1, i);
+#pragma unroll
+          for (int i = (tap - PUTD) * FPT; i >= 0 && i < (tap - PUTD + 1) * FPT && i < NF; ++i) fput(nxt, i);
           if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -606,8 +610,11 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
   #pragma unroll
         for (int tap = 0; tap < KK; ++tap) {
           ldw(fr[(tap + 2) % 3], ch * KK + tap + 2);
-          if (tap < NF) fload(ch + 1, tap);   // past the last chunk: c4 >= Cin4, zero reads into the idle buffer
-          if (tap >= PUTD && tap - PUTD < NF) fput(nxt, tap - PUTD);
+          // past the last chunk: c4 >= Cin4, zero reads into the idle buffer
+#pragma unroll
+          for (int i = tap * FPT; i < (tap + 1) * FPT && i < NF; ++i) fload(ch + 1, i);
+#pragma unroll
+          for (int i = (tap - PUTD) * FPT; i >= 0 && i < (tap - PUTD + 1) * FPT && i < NF; ++i) fput(nxt, i);
           if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
           __builtin_amdgcn_sched_barrier(0);
   #pragma unroll
@@ -1780,6 +1787,20 @@ static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
     return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true>(p, st);
   }
 }
+// x6 operands for the k3 s2 forwards (cheng2020 g_a.2 / g_a.4 conv1: leaky ReLU, and bias): one row per wave, the
+// fill two quads per tap
+template <int IT>
+static int pick_down_x6o_s2(const ConvParams& p, int epi, int fx, hipStream_t st) {
+  if (fx != 0) return -4;
+  const bool w32 = p.Wout >= 32 && p.Wout % 32 == 0;
+  if (epi == EPI_LRELU)
+    return w32 ? launch_down<3, 2, IT, 16, 32, EPI_LRELU, 0, false, true>(p, st)
+               : launch_down<3, 2, IT, 16, 16, EPI_LRELU, 0, false, true>(p, st);
+  if (epi == EPI_BIAS)
+    return w32 ? launch_down<3, 2, IT, 16, 32, EPI_BIAS, 0, false, true>(p, st)
+               : launch_down<3, 2, IT, 16, 16, EPI_BIAS, 0, false, true>(p, st);
+  return -4;
+}
 template <int IT, int EPI>
 static int pick_fx_down_x6o(const ConvParams& p, int fx, hipStream_t st) {
   switch (fx) {
@@ -2362,6 +2383,11 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
                  (a->fill_mode == 2 ? FX_UNSHUF : 0) | (a->save_t ? FX_T : 0);
   if (a->prec == 2) {
     if (a->kind == 0 && a->KS == 3 && a->S == 1) return pick_down_x6o(p, it, a->epi, fx, st);
+    if (a->kind == 0 && a->KS == 3 && a->S == 2 && a->fill_mode == 0 && !a->ps) {
+      if (it == 6) return pick_down_x6o_s2<6>(p, a->epi, fx, st);
+      if (it == 4) return pick_down_x6o_s2<4>(p, a->epi, fx, st);
+      return -4;
+    }
     return ica_conv_x6_dispatch(p, a->kind, a->KS, a->S, it, a->epi, fx, st);
   }
   if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, fx, st);

@@ -93,6 +93,9 @@ class Conv3:
         if x6 and stride == 2 and self.KS == 3 and not fwd_only and self.Cin in (128, 192) and self.it_b in X6_IT:
             # the k3 s2 input gradient (x6 conv_up, ica_conv_x6.hip pick_up3s2_x6): conv_up fragment order
             self.bwd6 = K.pack_conv_x6(w, self.Cin, self.Cout, 3, KK, self.Cin * KK, K.ORDER_UP, self.it_b)
+        if x6 and stride == 2 and self.KS == 3 and self.Cin >= 16 and mask is None and self.it in X6_IT:
+            # the k3 s2 forward (cheng2020 g_a.2 / g_a.4 conv1, leaky ReLU; ica_conv.hip pick_down_x6o_s2)
+            self.fwd6 = K.pack_conv_x6(w, self.Cout, self.Cin, 3, self.Cin * KK, KK, K.ORDER_DOWN, self.it)
         if x6 and stride == 1 and self.KS == 3 and self.Cin >= 16 and mask is None and self.it in X6_IT:
             self.fwd6 = K.pack_conv_x6(w, self.Cout, self.Cin, 3, self.Cin * KK, KK, K.ORDER_DOWN, self.it)
             if not fwd_only and self.Cout >= 16 and self.it_b in X6_IT:

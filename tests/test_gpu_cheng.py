@@ -80,6 +80,26 @@ def test_stride2_conv_input_gradient_x6(K, H, W, res):
     assert rel_err(got, ref) < 2e-6
 
 
+@pytest.mark.parametrize("H,W", [(64, 96), (66, 94), (256, 384), (30, 34)])
+def test_stride2_conv_forward_x6(K, H, W):
+    """The x6 forward of the stride-2 conv3x3 (cheng2020 g_a.2 / g_a.4 conv1: the X6O conv_down at S = 2, its 2.5x
+    larger patch filled two quads per tap; 32- and 16-px-wide tiles, tiles cut by the image edge, odd input sides)
+    with the bias and leaky-ReLU epilogues, against float64 at the fp32 tolerance."""
+    from imagecompression_adversarial_amd.engine_cheng import Conv3
+    C = 192
+    w = rnd((C, C, 3, 3), 25) / (C * 9) ** 0.5
+    b = rnd((C,), 26) * 0.1
+    c = Conv3(w.to(DEV), b.to(DEV), 2, x6=True)
+    assert c.fwd6 is not None
+    x = rnd((2, C, H, W), 27)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1)
+    x4 = K.to_nc4(x.to(DEV))
+    got = K.from_nc4(c.forward(x4, K.EPI_BIAS), C).cpu().double()
+    assert rel_err(got, ref) < 2e-6
+    got = K.from_nc4(c.forward(x4, K.EPI_LRELU), C).cpu().double()
+    assert rel_err(got, F.leaky_relu(ref, 0.01)) < 2e-6
+
+
 @pytest.mark.parametrize("H,W,Cg", [(64, 64, 192), (66, 94, 192), (63, 97, 128), (30, 62, 16)])
 def test_rgb_block_input_gradient_fused_x6(K, H, W, Cg):
     """cheng2020 g_a.0 (ResidualBlockWithStride(3, N)): the fused x6 input gradient conv3x3_s2^T(g1) + conv1x1_s2^T(gs)
