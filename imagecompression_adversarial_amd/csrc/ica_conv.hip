@@ -537,7 +537,8 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
 #pragma unroll
     for (int i = 0; i < NF; ++i) fput(patch, i);
     __syncthreads();
-    if constexpr (PT == 2) {
+    if constexpr (PT == 2 || S == 2) {
+      // (S = 2: the stride-2 forward's 10 fill quads per thread leave no room for a third weight set either)
       // Two 32-px rows per wave (the k3 layers on large grids): each weight fragment -- the main loop's
       // L1 -> register stream, ~37 B/cycle/CU at one row -- feeds twice the MFMAs.  The 2 x IT accumulators leave
       // room for two weight sets only, so the ring is a ping-pong one tap ahead; KK is odd, so a chunk's first set

@@ -28,6 +28,8 @@ from imagecompression_adversarial_amd.engine_cheng import Conv3  # noqa: E402
 gd = K.PackedGDN(torch.ones(N, device=dev) * 1.01, (0.1 * torch.eye(N, device=dev) + 0.001).sqrt())
 cv = Conv3(r(N, N, 3, 3) * 0.02, r(N) * 0.1, 1, x6=True)
 assert cv.fwd6 is not None and cv.bwd6 is not None
+cv2 = Conv3(r(N, N, 3, 3) * 0.02, r(N) * 0.1, 2, x6=True)
+assert cv2.fwd6 is not None
 
 
 def nc4(lo, hi):
@@ -47,6 +49,8 @@ cases = {
     "k3 masked lrelu_bwd": lambda: cv.dgrad(x, K.EPI_LRELU_BWD, fill_mode=K.FILL_LRELU_MASK, mask=m, saved=(a1, None)),
     "k3 gdn_bwd": lambda: cv.dgrad(x, K.EPI_GDN_BWD, gdn=gd, res=res, save_x=gs, saved=(sx, ss)),
     "k3 igdn_bwd": lambda: cv.dgrad(x, K.EPI_IGDN_BWD, gdn=gd, res=res, save_x=gs, saved=(sx, ss)),
+    # g_a.2 conv1: k3 stride 2 (256x384 -> 128x192), leaky ReLU (a quarter of the other cases' FLOPs)
+    "k3s2 lrelu": lambda: cv2.forward(x, K.EPI_LRELU),
 }
 cases = {k: f for k, f in cases.items() if only in k}
 times = {k: [] for k in cases}
@@ -62,7 +66,8 @@ for rnd in range(5):
         del out
 for k, v in times.items():
     ms = statistics.median(v)
-    print(f"{k:22s} {ms:7.3f} ms  {flop / ms / 1e9:7.1f} TFLOP/s (conv only)", flush=True)
+    fl = flop / 4 if "s2" in k else flop
+    print(f"{k:22s} {ms:7.3f} ms  {fl / ms / 1e9:7.1f} TFLOP/s (conv only)", flush=True)
 if "--dump" in sys.argv:
     dump = {}
     for k, f in cases.items():
