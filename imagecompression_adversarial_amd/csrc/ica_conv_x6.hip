@@ -771,6 +771,7 @@ ICA_DEV void conv_up_x6_class(const ConvParams& p, const f32x4* patch, int jt, i
   constexpr int KY0 = (PY + PAD) & 1, KX0 = (PX + PAD) & 1;
   constexpr int NY = (KS - KY0 + 1) / 2, NX = (KS - KX0 + 1) / 2, NT = NY * NX;
   constexpr int NCG = CG / 16;   // 16-channel chunks per LDS group
+  if constexpr (NT == 0) return;  // KS = 1: only class (0, 0) has a tap (the others' outputs are the epilogue's alone)
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int a_rel = jt * 2 * PT + (j >> 4), b_rel = j & 15;
   const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
@@ -1968,21 +1969,22 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
   return launch_up_x6_pt<IT, EPI, CG, X6_PT>(p, st);
 }
 
-// the k3 s2 input gradients of cheng2020's stride-2 residual blocks (conv_ex kind 1, x6): bias (+ residual) epilogue
-template <int IT, int FX, int CG, int PT>
+// the k3 s2 input gradients of cheng2020's stride-2 residual blocks (conv_ex kind 1, x6): bias (+ residual) epilogue;
+// KS = 1: the 1x1 stride-2 skips' input gradients (one tap in class (0, 0), zeros elsewhere)
+template <int IT, int FX, int CG, int PT, int KS = 3>
 int launch_up3s2_x6_pt(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<PT>() - 1) / xu_th<PT>()) * p.N;
   const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
-  const long ps = (long)ncb * 9 * (p.Cin / 16) * IT * 64;
+  const long ps = (long)ncb * KS * KS * (p.Cin / 16) * IT * 64;
   constexpr size_t lds = xu_lds_bytes<CG, PT>();
   static_assert(lds <= 160 * 1024, "conv_up_x6 channel group exceeds LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6_kernel<IT, EPI_BIAS, CG, PT, 3, FX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_up_x6_kernel<IT, EPI_BIAS, CG, PT, KS, FX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  ICA_LAUNCH((conv_up_x6_kernel<IT, EPI_BIAS, CG, PT, 3, FX>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
+  ICA_LAUNCH((conv_up_x6_kernel<IT, EPI_BIAS, CG, PT, KS, FX>), dim3(tiles, ncb), dim3(256), lds, st, p, ps);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -2044,6 +2046,13 @@ int pick_up_x6(const ConvParams& p, hipStream_t st) {
 // here; hip_ops.x6_ok restates this coverage so that PackedConv keeps the fp32 pack for such layers.
 int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, int epi, int fx, hipStream_t st) {
   if (kind == 1 && KS == 3 && S == 2) return pick_up3s2_x6(p, it, epi, fx, st);
+  if (kind == 1 && KS == 1 && S == 2) {   // cheng2020's 1x1 stride-2 skips (no residual)
+    if (epi != EPI_BIAS || fx != 0 || p.Cout % 32 != 0) return -4;
+    if (p.Hout != 2 * p.Hin || p.Wout != 2 * p.Win || (p.pl & (PL_IN | PL_OUT))) return -2;
+    if (it == 6 && p.Cin == 192) return launch_up3s2_x6_pt<6, 0, 192, 1, 1>(p, st);
+    if (it == 4 && p.Cin == 128) return launch_up3s2_x6_pt<4, 0, 128, 2, 1>(p, st);
+    return -3;
+  }
   if (KS != 5 || S != 2 || fx != 0) return -4;
   if (p.Cout % 32 != 0) return -4;
   if (kind == 0) {

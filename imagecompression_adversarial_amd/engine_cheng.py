@@ -90,9 +90,11 @@ class Conv3:
         # x6 operands (fp32-accurate bf16x6) for the k3 s1 layers: three-plane packs of the same fragment orders
         # (the input gradient's taps reversed by flipping the weight); launches that write t keep the fp32 packs
         self.fwd6 = self.bwd6 = None
-        if x6 and stride == 2 and self.KS == 3 and not fwd_only and self.Cin in (128, 192) and self.it_b in X6_IT:
-            # the k3 s2 input gradient (x6 conv_up, ica_conv_x6.hip pick_up3s2_x6): conv_up fragment order
-            self.bwd6 = K.pack_conv_x6(w, self.Cin, self.Cout, 3, KK, self.Cin * KK, K.ORDER_UP, self.it_b)
+        if (x6 and stride == 2 and self.KS in (1, 3) and not fwd_only and self.Cin in (128, 192)
+                and self.it_b in X6_IT):
+            # the k3 s2 input gradient (x6 conv_up, ica_conv_x6.hip pick_up3s2_x6) and the 1x1 s2 skips' (one tap in
+            # output class (0, 0)): conv_up fragment order
+            self.bwd6 = K.pack_conv_x6(w, self.Cin, self.Cout, self.KS, KK, self.Cin * KK, K.ORDER_UP, self.it_b)
         if x6 and stride == 2 and self.KS == 3 and self.Cin >= 16 and mask is None and self.it in X6_IT:
             # the k3 s2 forward (cheng2020 g_a.2 / g_a.4 conv1, leaky ReLU; ica_conv.hip pick_down_x6o_s2)
             self.fwd6 = K.pack_conv_x6(w, self.Cout, self.Cin, 3, self.Cin * KK, KK, K.ORDER_DOWN, self.it)
@@ -180,7 +182,7 @@ class ChengAnalysis:
             if i % 2 == 0:
                 self.blocks.append(("rbs", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 2, x6=x6),
                                     Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6),
-                                    Conv3(sd[f"{pre}.skip.weight"], sd[f"{pre}.skip.bias"], 2),
+                                    Conv3(sd[f"{pre}.skip.weight"], sd[f"{pre}.skip.bias"], 2, x6=x6),
                                     _gdn(sd, f"{pre}.gdn")))
             else:
                 self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6),

@@ -80,6 +80,24 @@ def test_stride2_conv_input_gradient_x6(K, H, W, res):
     assert rel_err(got, ref) < 2e-6
 
 
+@pytest.mark.parametrize("H,W", [(64, 96), (96, 160), (256, 384)])
+def test_stride2_skip_input_gradient_x6(K, H, W):
+    """The x6 input gradient of the 1x1 stride-2 skip (cheng2020 g_a.2 / g_a.4 skip: conv_up_x6 at KS = 1, one tap in
+    output class (0, 0), zeros elsewhere) against float64 autograd at the fp32 tolerance."""
+    from imagecompression_adversarial_amd.engine_cheng import Conv3
+    C = 192
+    w = rnd((C, C, 1, 1), 28) / C ** 0.5
+    b = rnd((C,), 29) * 0.1
+    c = Conv3(w.to(DEV), b.to(DEV), 2, x6=True)
+    assert c.bwd6 is not None
+    g = rnd((2, C, H // 2, W // 2), 30)
+    x = torch.zeros((2, C, H, W), dtype=torch.float64, requires_grad=True)
+    F.conv2d(x, w.double(), b.double(), stride=2).backward(g.double())
+    got = K.from_nc4(c.dgrad(K.to_nc4(g.to(DEV))), C).cpu().double()
+    assert rel_err(got, x.grad) < 2e-6
+    assert float(got[:, :, 1::2].abs().max()) == 0.0 and float(got[:, :, :, 1::2].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("H,W", [(64, 96), (66, 94), (256, 384), (30, 34)])
 def test_stride2_conv_forward_x6(K, H, W):
     """The x6 forward of the stride-2 conv3x3 (cheng2020 g_a.2 / g_a.4 conv1: the X6O conv_down at S = 2, its 2.5x
