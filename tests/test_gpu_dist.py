@@ -23,12 +23,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _inputs(B=4):
+MODELS = {"hyper": (192, 128), "cheng2020": (128, 128)}   # (M, N) at quality 3
+
+
+def _inputs(B=4, model="hyper"):
+    M, N = MODELS[model]
     g = torch.Generator().manual_seed(7)
     x = torch.rand((B, 3, H, W), generator=g)
-    ny = torch.rand((B, 192, H // 16, W // 16), generator=g) - 0.5
-    nz = torch.rand((B, 128, H // 64, W // 64), generator=g) - 0.5
+    ny = torch.rand((B, M, H // 16, W // 16), generator=g) - 0.5
+    nz = torch.rand((B, N, H // 64, W // 64), generator=g) - 0.5
     return x, ny, nz
+
+
+def _net(model):
+    from imagecompression_adversarial_amd import codec, coder
+    net = codec.bmshj2018_hyperprior(3) if model == "hyper" else codec.cheng2020_anchor(3)
+    coder._synthetic_init(net, seed=0)
+    return net
 
 
 def _args():
@@ -36,17 +47,15 @@ def _args():
                            round_adv=False)
 
 
-def _one_step(rank, world, group, B=4):
-    from imagecompression_adversarial_amd import codec, coder
+def _one_step(rank, world, group, B=4, model="hyper"):
+    from imagecompression_adversarial_amd import coder
     from imagecompression_adversarial_amd.train import adv_step
     from imagecompression_adversarial_amd.train_engine import RDTrainer
     from imagecompression_adversarial_amd import dist as D
-    net = codec.bmshj2018_hyperprior(3)
-    coder._synthetic_init(net, seed=0)
-    net = net.to("cuda:0").train()
+    net = _net(model).to("cuda:0").train()
     opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=1e-4))
     tr = RDTrainer(net, "mse", 0.0130)
-    x, ny, nz = _inputs(B)
+    x, ny, nz = _inputs(B, model)
     sl = D.shard_range(B, rank, world)
     sh = slice(sl.start, sl.stop)
     out, _ = adv_step(net, tr, opt, aux, x[sh].cuda(), _args(), group, world,
@@ -56,7 +65,7 @@ def _one_step(rank, world, group, B=4):
     return flat, float(out["loss"])
 
 
-def _worker(rank, world, port, q, B=4):
+def _worker(rank, world, port, q, B=4, model="hyper"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
@@ -64,7 +73,7 @@ def _worker(rank, world, port, q, B=4):
         from imagecompression_adversarial_amd import dist as D
         torch.cuda.set_device(0)
         r, w, group = D.init_from_env("gloo")
-        flat, loss = _one_step(r, w, group, B)
+        flat, loss = _one_step(r, w, group, B, model)
         q.put((rank, flat, loss, None))
     except Exception as e:  # surface failures to the parent
         q.put((rank, None, None, repr(e)))
@@ -73,15 +82,16 @@ def _worker(rank, world, port, q, B=4):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nb", [(2, 4), (3, 5)])
-def test_dp_adv_step_matches_single_process(world, nb):
+@pytest.mark.parametrize("world,nb,model", [(2, 4, "hyper"), (3, 5, "hyper"), (2, 4, "cheng2020")])
+def test_dp_adv_step_matches_single_process(world, nb, model):
     """(3, 5): uneven shards 1/2/2: every rank's gradient and loss are weighted by its share of
-    the global batch, so the step still equals the whole-batch step."""
-    ref_flat, ref_loss = _one_step(0, 1, None, nb)
+    the global batch, so the step still equals the whole-batch step.  cheng2020: the joint-prior train step
+    (train_cheng) under the same data-parallel outer step."""
+    ref_flat, ref_loss = _one_step(0, 1, None, nb, model)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, nb)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, nb, model)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -94,7 +104,7 @@ def test_dp_adv_step_matches_single_process(world, nb):
     for r in range(1, world):
         assert torch.equal(res[0][0], res[r][0]), "replicas diverged"
     d = (res[0][0] - ref_flat).abs().max().item()
-    moved = (ref_flat - _init_flat()).abs().max().item()
+    moved = (ref_flat - _init_flat(model)).abs().max().item()
     assert moved > 0
     assert d <= 2e-3 * moved, (d, moved)
     # every rank reports the whole-batch loss (shard means weighted by shard size, summed)
@@ -102,8 +112,5 @@ def test_dp_adv_step_matches_single_process(world, nb):
         assert abs(res[r][1] - ref_loss) <= 1e-3 * abs(ref_loss)
 
 
-def _init_flat():
-    from imagecompression_adversarial_amd import codec, coder
-    net = codec.bmshj2018_hyperprior(3)
-    coder._synthetic_init(net, seed=0)
-    return torch.cat([p.detach().flatten() for p in net.parameters()])
+def _init_flat(model="hyper"):
+    return torch.cat([p.detach().flatten() for p in _net(model).parameters()])
