@@ -169,6 +169,35 @@ def _dist_env():
     return world, rank, dev, dist
 
 
+def _rank_stats(dist, dev, el, units, world, extra=None):
+    """Per-rank evidence for the N > 1 line (the driver's 8-GPU run): the backend and world size the process group
+    actually initialised, every rank's own elapsed time over the timed steps (gathered BEFORE the MAX that sets
+    `value`), its device and work units, and the spread.  `extra` (per rank, float): e.g. the fine-tune's
+    all-reduce milliseconds per outer step."""
+    vals = [float(el), float(units), float(dev.index if dev.index is not None else -1), float(extra or 0.0)]
+    if dist is None:
+        rows = [vals]
+        backend, ws = None, 1
+    else:
+        backend = str(dist.get_backend())
+        # gloo gathers host tensors (its CUDA support covers all_reduce / broadcast only)
+        t = torch.tensor(vals, device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        rows = [p.tolist() for p in parts]
+        ws = dist.get_world_size()
+    els = [r[0] for r in rows]
+    out = {"backend": backend, "world_size": ws,
+           "rank_elapsed_s": [round(e, 4) for e in els],
+           "rank_value": [round(r[1] / r[0], 3) if r[0] > 0 else None for r in rows],
+           "rank_device": [int(r[2]) for r in rows],
+           "elapsed_min_s": round(min(els), 4), "elapsed_max_s": round(max(els), 4),
+           "imbalance": round(max(els) / min(els) - 1.0, 4) if min(els) > 0 else None}
+    if extra is not None:
+        out["rank_extra"] = [round(r[3], 4) for r in rows]
+    return out
+
+
 def _kernel_table(hook, flops_img):
     tot_ms = {tag: sum(a.elapsed_time(b) for a, b, _ in evs) for tag, evs in hook.items()}
     tot_fl = {tag: sum(flops_img[tag] * n for _, _, n in evs) for tag, evs in hook.items()}
@@ -283,6 +312,7 @@ def bench_finetune(args):
     K.FLOPS_HOOK = {}
     K.PREC_HOOK = {}
     K.LAUNCH_HOOK = {}
+    D.COLL_HOOK = {} if dist else None
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         adv_step(net, tr, opt, aux, xs[i], fargs, group, world)
@@ -290,9 +320,13 @@ def bench_finetune(args):
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    coll, D.COLL_HOOK = D.COLL_HOOK, None
+    # all-reduce time per outer step (HIP events around each collective on the issuing stream)
+    coll_ms = {k: sum(a.elapsed_time(b) for a, b in v) / args.steps for k, v in (coll or {}).items()}
     hook, K.EVENT_HOOK = K.EVENT_HOOK, None
     table = _launch_table(K.LAUNCH_HOOK, rank)
     K.LAUNCH_HOOK = None
+    ranks = _rank_stats(dist, dev, el, B * inner * args.steps, world, extra=coll_ms.get("grad", 0.0) if dist else None)
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -332,6 +366,9 @@ def bench_finetune(args):
                        "per_gpu_batch": B, "global_batch": B * world, "height": H, "width": W,
                        "parallelism": f"data-parallel x{world}, one flat grad all-reduce per outer step"},
             "outer_steps_per_s": round(args.steps / el, 4),
+            "distributed": dict(ranks, **({"allreduce_ms_per_outer_step": {k: round(v, 4) for k, v in coll_ms.items()},
+                                           "rank_extra_is": "flat-gradient all-reduce ms per outer step"}
+                                          if dist else {})),
             "roofline": roof(dom), "wgrad_roofline": roof(wdom),
             "per_kernel_ms_total_per_outer_step": {k: round(v / args.steps, 3) for k, v in sorted(tot_ms.items())},
             "cpu_baseline": (None if world > 1 or args.no_cpu_baseline else
@@ -454,6 +491,7 @@ def main():
     table = _launch_table(K.LAUNCH_HOOK, rank)
     K.LAUNCH_HOOK = None
     exp_steps = loop.expensive_image_steps() - exp0   # image-steps of the timed window that ran the network
+    ranks = _rank_stats(dist, dev, el, B * args.steps, world)
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -564,6 +602,7 @@ def main():
                          "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
             "branch_census": {"expensive_image_steps": exp_steps, "image_steps": B * args.steps,
                               "expensive_frac": round(exp_steps / (B * args.steps), 4)},
+            "distributed": ranks,
             "full_run": full,
             "mixed_branch_run": mixed,
             "step_gflop_per_image": round(total_flops / B / 1e9, 2),

@@ -156,7 +156,8 @@ inline int ica_cu_count() {
 struct IcaLaunchRec {
   const void* fn;
   unsigned long long threads;   // grid x block, as rocprofv3's Grid_Size
-  int count;                    // launches since the record was last consumed
+  int count;                    // launches since the record was last consumed, saturated at 2 (callers need 0 / 1 /
+                                // many; a hook-less run never consumes it)
 };
 inline IcaLaunchRec& ica_launch_rec() {
   static thread_local IcaLaunchRec r{nullptr, 0, 0};
@@ -172,7 +173,7 @@ inline const void* ica_fnptr(F* f) {   // a kernel (function designator or point
     IcaLaunchRec& ica_r_ = ica_launch_rec();                                                                 \
     ica_r_ = IcaLaunchRec{ica_fnptr(kern),                                                                   \
                           (unsigned long long)ica_g_.x * ica_g_.y * ica_g_.z * ica_b_.x * ica_b_.y * ica_b_.z, \
-                          ica_r_.count + 1};                                                                 \
+                          ica_r_.count < 2 ? ica_r_.count + 1 : 2};                                          \
     hipLaunchKernelGGL(kern, ica_g_, ica_b_, lds, st, __VA_ARGS__);                                          \
   } while (0)
 

@@ -557,194 +557,334 @@ __global__ __launch_bounds__(512, 1) void conv_down_x6w_kernel(ConvParams p, lon
 }
 
 // --------------------------------------------------------------------------------------------------------------
-// conv_rgb_x6: the k5 s2 conv whose input is an RGB-sized map (Cin <= 4: g_a.0 forward, the g_s.6 input gradient)
-// as its PixelUnshuffle(2) view: a k3 s1 p1 conv over 16 virtual channels c' = 4 (2 sy + sx) + c at the output
-// resolution, x'[c'][u][v] = x[c][2u + sy][2v + sx]; the weight (ica_pack_conv_weight_x6 of w'[o][c'][ty][tx] =
-// w[o][c][2 ty + sy][2 tx + sx], zero where 2 ty + sy or 2 tx + sx is 5) covers the 5 x 5 taps with 3 x 3.  K is
-// 9 steps of 16 (vs 25 x 4 channels): the kernel is epilogue- and store-heavy, so it runs 2 blocks per CU with one
-// 32-pixel tile per wave, the fill / epilogue of one block overlapping the MFMAs of the other.
+// conv_rgb5_x6: the k5 s2 conv whose input is a 3-channel map (g_a.0 forward, the g_s.6 input gradient; 128 output
+// channels), with its 75 (tap, channel) pairs packed densely into K: 5 steps of 16, one per tap row ky (the
+// PixelUnshuffle(2) k3 view of rounds 2-5 ran 9 steps of 16 for the same 75 pairs: 1.92x the MFMA work).  k = 8 h + e
+// of step ky is
+//     h = 0: e 0-5 -> (kx 0, c 0-2), (kx 1, c 0-2);   e 6, 7 -> (kx 4, c 0), (kx 4, c 1)
+//     h = 1: e 0-5 -> (kx 2, c 0-2), (kx 3, c 0-2);   e 6    -> (kx 4, c 2);  e 7: zero weight
+// so the B fragment of lane (h, j) (output pixel ox = ox0 + j) is built in registers from three RGB quads of input
+// row 2 oy + ky - 2: columns 2 ox - 2 + 2 h, 2 ox - 1 + 2 h and 2 ox + 2 (one 16-B load each; padding reads past
+// the descriptor and returns zeros), split into its three bf16 planes.  A wave computes one 32-pixel output row.
+//   Everything the tiles share lives in LDS for the whole launch: the conv weight fragments (3 planes x 5 steps x 4
+// row tiles, 60 KB), the x6 gamma' / gamma'^T pack (96 KB), bias and beta' (1 KB) -- 157 KB, one persistent block
+// per CU walking a contiguous run of row tiles.  Streamed from L2 per tile instead, those 156 KB of fragments per
+// 32-pixel row outran the vector L1 (the per-tile form ran 1.31 / 1.65 ms at the config-2 shapes).
+// Weights: [plane][ky][it][lane][e] (pack_conv_rgb5_x6_kernel, ica_pack_conv_weight_x6 order 2), plane stride ps.
 // --------------------------------------------------------------------------------------------------------------
-template <int IT, int EPI>
-__global__ __launch_bounds__(256, 2) void conv_rgb_x6_kernel(ConvParams p, long ps) {
-  constexpr int KK = 9, TW = 32, TH = 4, PR = TH + 2, PC = TW + 2, PLANE = PR * PC;
-  constexpr int NF = (4 * PLANE + 255) / 256;
-  __shared__ f32x4 patch[3 * 2 * PLANE];   // [plane][half][pixel]: virtual channels 8h..8h+7 as bf16
-  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
-  int bid, cb;
-  xcd_block<true>(bid, cb);
-  const int tx = bid % tiles_x;
-  bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int n = bid / tiles_y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  f32x16 acc[IT];
-#pragma unroll
-  for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
-  // fill: entry e = (sub-pixel quad q, patch pixel) <- RGB quad of input pixel (2u + sy, 2v + sx); padding and
-  // pixels past the image read out of the descriptor's range (zeros); channel lane 3 is the nChw4c zero pad
+constexpr int RGB5_KY = 5, RGB5_IT = 4;
+#ifndef RGB5_AB
+#define RGB5_AB 0   // timing-only A/B builds (scripts/build_variant.sh): 1 = 1/16 of the forward stores, 2 = no GDN GEMM
+#endif
+constexpr int RGB5_W_BYTES = 3 * RGB5_KY * RGB5_IT * 64 * 16;            // 61440
+constexpr int RGB5_G_BYTES = 3 * RGB5_IT * RGB5_IT * 2048;               // 98304
+constexpr int RGB5_LDS = RGB5_W_BYTES + RGB5_G_BYTES + 2 * 128 * 4;      // + bias, beta': 160768
+
+// the 15 input quads of one output pixel's 5 tap rows (lane half h's columns)
+ICA_DEV void rgb5_load(const ConvParams& p, int n, int oy, int ox, bool valid, f32x4 (&q)[RGB5_KY][3]) {
+  const int h = (threadIdx.x & 63) >> 5;
   const __amdgpu_buffer_rsrc_t xr =
       uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * p.Hin * p.Win * 16, (unsigned)p.Hin * p.Win * 16u);
-  f32x4 v[NF];
+  const int c0 = 2 * ox - 2 + 2 * h, c2 = 2 * ox + 2;
+  const int cols[3] = {c0, c0 + 1, c2};
 #pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    const int e = threadIdx.x + 256 * i;
-    const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
-    const int iy = 2 * (oy0 - 1 + pr) + (q >> 1), ix = 2 * (ox0 - 1 + pc) + (q & 1);
-    const bool ok = e < 4 * PLANE && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const unsigned vo = ((unsigned)iy * p.Win + ix) * 16u;
-    v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+  for (int ky = 0; ky < RGB5_KY; ++ky) {
+    const int iy = 2 * oy + ky - 2;
+    const bool rok = valid && iy >= 0 && iy < p.Hin;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const bool ok = rok && cols[k] >= 0 && cols[k] < p.Win;
+      const unsigned vo = ((unsigned)iy * p.Win + cols[k]) * 16u;
+      q[ky][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
+    }
   }
+}
+
+ICA_DEV bf16x8 lds_frag(const char* lds, int off) { return *reinterpret_cast<const bf16x8*>(lds + off); }
+
+// block prologue: the weight planes, the gamma' pack (GDN epilogues), bias and beta' into LDS (layout above)
+template <bool GDN>
+ICA_DEV void rgb5_stage(const ConvParams& p, long ps, char* lds) {
   const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
-  const int wbase = cb * KK * IT * 64;
+  const __amdgpu_buffer_rsrc_t gr = uniform_rsrc(GDN ? p.gp : nullptr, GDN ? RGB5_G_BYTES : 0);
+  const __amdgpu_buffer_rsrc_t br = chan_rsrc(p.bias, p.Cout), er = chan_rsrc(GDN ? p.beta : nullptr, p.Cout);
+  constexpr int NW = RGB5_W_BYTES / 16, NG = GDN ? RGB5_G_BYTES / 16 : 0, NE = NW + RGB5_G_BYTES / 16 + 64;
+  for (int e = threadIdx.x; e < NE; e += blockDim.x) {
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e < NW) {   // plane pl, byte b of the plane
+      const int pl = e / (NW / 3), b = (e - pl * (NW / 3)) * 16;
+      v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, (int)(pl * ps * 16) + b, 0, 0));
+    } else if (e < NW + RGB5_G_BYTES / 16) {
+      if (NG) v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(gr, (e - NW) * 16, 0, 0));
+    } else {
+      const int k = e - NW - RGB5_G_BYTES / 16;   // 0-31 bias quads, 32-63 beta' quads
+      v = k < 32 ? ld_chan4(br, 4 * k) : ld_chan4(er, 4 * (k - 32));
+    }
+    *reinterpret_cast<f32x4*>(lds + (size_t)e * 16) = v;
+  }
+  __syncthreads();
+}
+
+// the 5-step main loop, weight fragments from LDS one step ahead
+ICA_DEV void rgb5_main(const char* lds, const f32x4 (&q)[RGB5_KY][3], f32x16 (&acc)[RGB5_IT]) {
+  constexpr int IT = RGB5_IT, PS = RGB5_W_BYTES / 3;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
   auto ldw = [&](bf16x8 (&a)[IT][3], int g) {
-    const int f = wbase + g * IT * 64;
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+      for (int pl = 0; pl < 3; ++pl) a[it][pl] = lds_frag(lds, pl * PS + ((g * IT + it) * 64 + lane) * 16);
   };
   bf16x8 fa[IT][3], fb[IT][3];
   ldw(fa, 0);
-  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
+  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int ky) __attribute__((always_inline)) {
+    if (ky + 1 < RGB5_KY) ldw(nxt, ky + 1);
+    __builtin_amdgcn_sched_barrier(0);   // the scheduler otherwise hoists every step's LDS reads (spills)
+    const f32x4 a = q[ky][0], b = q[ky][1], c = q[ky][2];
+    const float v[8] = {a[0], a[1], a[2], b[0], b[1], b[2], h ? c[2] : c[0], h ? 0.f : c[1]};
+    bf16x8 bs[3];
+    split3x8(v, bs);
 #pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    const int e = threadIdx.x + 256 * i;
-    if (e < 4 * PLANE) {
-      const int q = e / PLANE, pix = e - q * PLANE;
-      u32x2 a, b, c;
-      split3(v[i], a, b, c);
-      const int ent = (q >> 1) * PLANE + pix;
-      p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
-      p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
-      p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
-    }
-  }
-  __syncthreads();
-  auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) __attribute__((always_inline)) {
-    if (g + 1 < KK) ldw(nxt, g + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    const int ky = g / 3, kx = g - 3 * (g / 3);
-    const int o = h * PLANE + (wave + ky) * PC + j + kx;
-    const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
-#pragma unroll
-    for (int it = 0; it < IT; ++it) acc[it] = mfma_x6(cur[it], b, acc[it]);
+    for (int it = 0; it < IT; ++it) acc[it] = mfma_x6(cur[it], bs, acc[it]);
   };
 #pragma unroll
-  for (int g = 0; g < KK; ++g) {
-    if (g & 1) step(fb, fa, g);
-    else step(fa, fb, g);
+  for (int ky = 0; ky < RGB5_KY; ++ky) {
+    if (ky & 1) step(fb, fa, ky);
+    else step(fa, fb, ky);
   }
-  const int oy = oy0 + wave, ox = ox0 + j;
-  conv_epilogue<IT, EPI, 0, false, 2>(p, acc, n, oy, ox, oy < p.Hout && ox < p.Wout, cb * IT * 32);
 }
 
-// The GDN-backward form (g_s.6 input gradient): pipelined over a contiguous run of tiles per block, one block per CU
-// (the wide epilogue's t / 2x / g*s and u GEMM need the 512-register file): tile i+1's patch loads and tile i's
-// saved (y, s) loads are issued before tile i's main loop, so their HBM latency hides behind its MFMAs.  Every tile runs the same instruction sequence whichever block takes it (batch-independent bits).
-template <int IT, int EPI>
-__global__ __launch_bounds__(256, 1) void conv_rgb_bwd_x6_kernel(ConvParams p, long ps, int tiles_per_block) {
-  constexpr int KK = 9, TW = 32, TH = 4, PR = TH + 2, PC = TW + 2, PLANE = PR * PC;
-  constexpr int NF = (4 * PLANE + 255) / 256;
-  static_assert(EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD, "GDN-backward epilogues");
-  __shared__ f32x4 patch[3 * 2 * PLANE];   // [plane][half][pixel]: virtual channels 8h..8h+7 as bf16
-  const int tiles_x = (p.Wout + TW - 1) / TW, tiles_y = (p.Hout + TH - 1) / TH;
-  const int total = tiles_x * tiles_y * p.N;
-  int blk, cb;
-  xcd_block<true>(blk, cb);
-  const int t_begin = blk * tiles_per_block, t_end = min(total, t_begin + tiles_per_block);
-  if (t_begin >= t_end) return;   // block-uniform
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-  auto coords = [&](int t, int& n, int& oy0, int& ox0) {
-    const int tx = t % tiles_x, r = t / tiles_x;
-    oy0 = (r % tiles_y) * TH;
-    ox0 = tx * TW;
-    n = r / tiles_y;
-  };
-  // fill: entry e = (sub-pixel quad q, patch pixel) <- RGB quad of input pixel (2u + sy, 2v + sx); padding and
-  // pixels past the image read out of the descriptor's range (zeros); channel lane 3 is the nChw4c zero pad
-  auto load_patch = [&](int t, f32x4 (&v)[NF]) {
-    int n, oy0, ox0;
-    coords(t, n, oy0, ox0);
-    const __amdgpu_buffer_rsrc_t xr = uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * p.Hin * p.Win * 16,
-                                                   (unsigned)p.Hin * p.Win * 16u);
+// bias / GDN / IGDN forward epilogue of one row tile, parameters from LDS (narrow: 256 registers, one normaliser
+// tile at a time, x^2 split once per k-step; the ops and MFMA order of gdn_fwd_x6_tile_narrow)
+template <int EPI>
+ICA_DEV void rgb5_epi_fwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RGB5_IT], int n, int oy, int ox,
+                          bool valid) {
+  constexpr int IT = RGB5_IT;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+  const f32x4* bq = reinterpret_cast<const f32x4*>(lds + RGB5_W_BYTES + RGB5_G_BYTES);   // [32 bias][32 beta'] quads
+  const unsigned vo = h * plane + (valid ? pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u);
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int e = threadIdx.x + 256 * i;
-      const int q = e / PLANE, rem = e - q * PLANE, pr = rem / PC, pc = rem - pr * PC;
-      const int iy = 2 * (oy0 - 1 + pr) + (q >> 1), ix = 2 * (ox0 - 1 + pc) + (q & 1);
-      const bool ok = e < 4 * PLANE && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const unsigned vo = ((unsigned)iy * p.Win + ix) * 16u;
-      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? vo : 0xFFFFFFF0u, 0, 0));
-    }
-  };
-  u32x2* p2 = reinterpret_cast<u32x2*>(patch);
-  auto put_patch = [&](const f32x4 (&v)[NF]) {
+  for (int it = 0; it < IT; ++it)
 #pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      const int e = threadIdx.x + 256 * i;
-      if (e < 4 * PLANE) {
-        const int q = e / PLANE, pix = e - q * PLANE;
-        u32x2 a, b, c;
-        split3(v[i], a, b, c);
-        const int ent = (q >> 1) * PLANE + pix;
-        p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
-        p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
-        p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
-      }
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = bq[it * 8 + 2 * g + h];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[it][4 * g + e] += bv[e];
     }
-  };
-  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * ps * 16));
-  const int wbase = cb * KK * IT * 64;
-  // wbz: a per-tile "zero" the compiler cannot hoist, so the 108 scalar fragment offsets of the 9 steps are formed
-  // per step instead of being hoisted out of the tile loop into SGPRs (which spilled)
-  int wbz = 0;
-  auto ldw = [&](bf16x8 (&a)[IT][3], int g) {
-    const int f = wbase + g * IT * 64;
+  if constexpr (EPI == EPI_BIAS) {
+    if (valid) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          Y.st(vo, (unsigned)(it * 8 + 2 * g) * plane,
+               f32x4{acc[it][4 * g], acc[it][4 * g + 1], acc[it][4 * g + 2], acc[it][4 * g + 3]});
+    }
+    return;
+  } else {
+    const char* gl = lds + RGB5_W_BYTES;
+    bf16x8 xs2[IT][2][3];
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, wbz + (int)((q * ps + f + it * 64) * 16));
-  };
-  f32x4 v[NF];
-  load_patch(t_begin, v);
-  put_patch(v);
-  __syncthreads();
-#pragma unroll 1
-  for (int t = t_begin; t < t_end; ++t) {
-    int n, oy0, ox0;
-    coords(t, n, oy0, ox0);
-    wbz = 0;
-    asm volatile("" : "+s"(wbz));
-    const int oy = oy0 + wave, ox = ox0 + j;
-    const bool valid = oy < p.Hout && ox < p.Wout;
-    f32x4 yq[IT][4], sq[IT][4];
-    gdn_bwd_x6_load<IT>(p, n, oy, ox, valid, yq, sq);
-    const bool more = t + 1 < t_end;
-    if (more) load_patch(t + 1, v);
-    bf16x8 fa[IT][3], fb[IT][3];
-    ldw(fa, 0);
-    f32x16 acc[IT];
+      for (int s = 0; s < 2; ++s) {
+        float v[8];
 #pragma unroll
-    for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
-    auto step = [&](bf16x8 (&cur)[IT][3], bf16x8 (&nxt)[IT][3], int g) __attribute__((always_inline)) {
-      if (g + 1 < KK) ldw(nxt, g + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      const int ky = g / 3, kx = g - 3 * (g / 3);
-      const int o = h * PLANE + (wave + ky) * PC + j + kx;
-      const bf16x8 b[3] = {f4_as_bf8(patch[o]), f4_as_bf8(patch[2 * PLANE + o]), f4_as_bf8(patch[4 * PLANE + o])};
+        for (int j = 0; j < 8; ++j) v[j] = acc[it][8 * s + j] * acc[it][8 * s + j];
+        split3x8(v, xs2[it][s]);
+      }
+    auto ldg = [&](bf16x8 (&a)[3], int ct, int k) {
 #pragma unroll
-      for (int it = 0; it < IT; ++it) acc[it] = mfma_x6(cur[it], b, acc[it]);
+      for (int pl = 0; pl < 3; ++pl)
+        a[pl] = lds_frag(gl, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + pl * IT * IT * 2048 + lane * 16);
     };
 #pragma unroll
-    for (int g = 0; g < KK; ++g) {
-      if (g & 1) step(fb, fa, g);
-      else step(fa, fb, g);
+    for (int ct = 0; ct < IT; ++ct) {
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 nx;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 ev = bq[32 + ct * 8 + 2 * g + h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) nx[4 * g + e] = ev[e];
+      }
+      bf16x8 ga[2][3];
+#if RGB5_AB != 2
+      ldg(ga[0], ct, 0);
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], ct, k + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        nx = mfma_x6(ga[k & 1], xs2[k >> 1][k & 1], nx);
+      }
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      if (valid) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 yv, sv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float nv = nx[4 * g + e];
+            const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+            sv[e] = sc;
+            yv[e] = acc[ct][4 * g + e] * sc;
+          }
+          const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
+#if RGB5_AB == 1
+          if (ct == 0 && g == 0) {
+            if (p.save_s) SS.st(vo, ss, sv);
+            Y.st(vo, ss, yv);
+          }
+#else
+          if (p.save_s) SS.st(vo, ss, sv);
+          Y.st(vo, ss, yv);
+#endif
+        }
+      }
     }
-    __syncthreads();   // every wave is done with tile t's patch
-    if (more) put_patch(v);
-    gdn_bwd_x6_wide<IT, EPI>(p, acc, n, oy, ox, valid, yq, sq);
-    __syncthreads();   // tile t+1's patch is in LDS
+  }
+}
+
+// GDN / IGDN backward epilogue of one row tile (the wide form of gdn_bwd_x6_wide, 512 registers), gamma'^T
+// fragments from LDS one round ahead
+template <int EPI>
+ICA_DEV void rgb5_epi_bwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RGB5_IT], int n, int oy, int ox,
+                          bool valid, const f32x4 (&yq)[RGB5_IT][4], const f32x4 (&sq)[RGB5_IT][4]) {
+  constexpr int IT = RGB5_IT;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const Img4 Y(p.y, img, n);
+  const unsigned vo = valid ? h * plane + pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u;
+  f32x16 xx[IT];
+  bf16x8 tq[IT][2][3];
+  float tw[8];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 yv = yq[it][g], sv = sq[it][g];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sg = sv[e], rs = __builtin_amdgcn_rcpf(sg), xs = yv[e] * rs;
+        const float gx = acc[it][4 * g + e] * xs;
+        tw[4 * (g & 1) + e] = (EPI == EPI_GDN_BWD) ? (-0.5f * gx) * (sg * sg * sg) : (0.5f * gx) * rs;
+        float gs = acc[it][4 * g + e] * sg;
+        float x2 = 2.0f * xs;
+        asm volatile("" : "+v"(gs), "+v"(x2));
+        acc[it][4 * g + e] = gs;
+        xx[it][4 * g + e] = x2;
+      }
+      if (g & 1) split3x8(tw, tq[it][g >> 1]);
+    }
+  const char* gl = lds + RGB5_W_BYTES;
+  f32x16 ux[IT];
+#pragma unroll
+  for (int jt = 0; jt < IT; ++jt) ux[jt] = f32x16{0};
+  bf16x8 ga[2][IT][3];
+  auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
+#pragma unroll
+    for (int jt = 0; jt < IT; ++jt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[jt][pl] = lds_frag(gl, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + pl * IT * IT * 2048 + lane * 16);
+  };
+  __builtin_amdgcn_sched_barrier(0);
+  ldg(ga[0], 0);
+#pragma unroll
+  for (int k = 0; k < 2 * IT; ++k) {
+    if (k + 1 < 2 * IT) ldg(ga[(k + 1) & 1], k + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int jt = 0; jt < IT; ++jt) ux[jt] = mfma_x6(ga[k & 1][jt], tq[k >> 1][k & 1], ux[jt]);
+  }
+  if (valid) {
+#pragma unroll
+    for (int jt = 0; jt < IT; ++jt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[jt][4 * g + e] + xx[jt][4 * g + e] * ux[jt][4 * g + e];
+        Y.st(vo, (unsigned)(jt * 8 + 2 * g) * plane, v);
+      }
+  }
+}
+
+// forward (bias / GDN / IGDN): 8 waves (two per SIMD: one wave's loads and stores overlap the other's MFMAs), each
+// wave a sequence of row tiles
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void conv_rgb5_x6_kernel(ConvParams p, long ps, int nblk) {
+  extern __shared__ __attribute__((aligned(16))) char rgb5_lds[];
+  constexpr bool GDN = EPI == EPI_GDN || EPI == EPI_IGDN;
+  rgb5_stage<GDN>(p, ps, rgb5_lds);
+  const int tiles_x = (p.Wout + 31) / 32, total = tiles_x * p.Hout * p.N, per = (total + nblk - 1) / nblk;
+  int b, cb;
+  xcd_block<true>(b, cb);
+  const int t_end = min(total, b * per + per), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll 1
+  for (int t = b * per + wave; t < t_end; t += 8) {
+    const int tx = t % tiles_x, r = t / tiles_x;
+    const int oy = r % p.Hout, n = r / p.Hout, ox = tx * 32 + (threadIdx.x & 31);
+    const bool valid = ox < p.Wout;
+    f32x4 q[RGB5_KY][3];
+    rgb5_load(p, n, oy, ox, valid, q);
+    f32x16 acc[RGB5_IT];
+#pragma unroll
+    for (int it = 0; it < RGB5_IT; ++it) acc[it] = f32x16{0};
+    rgb5_main(rgb5_lds, q, acc);
+    rgb5_epi_fwd<EPI>(p, rgb5_lds, acc, n, oy, ox, valid);
+  }
+}
+
+// GDN / IGDN backward (g_s.6 input gradient): 4 waves (one per SIMD: the wide epilogue needs the 512-register file),
+// each a sequence of row tiles; tile i's saved (y, s) loads are issued before its main loop and tile i+1's input
+// quads before tile i's epilogue, so their HBM latency hides behind MFMAs.  Every tile runs the same instruction
+// sequence whichever wave takes it (batch-independent bits).
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void conv_rgb5_bwd_x6_kernel(ConvParams p, long ps, int nblk) {
+  extern __shared__ __attribute__((aligned(16))) char rgb5_lds[];
+  static_assert(EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD, "GDN-backward epilogues");
+  rgb5_stage<true>(p, ps, rgb5_lds);
+  const int tiles_x = (p.Wout + 31) / 32, total = tiles_x * p.Hout * p.N, per = (total + nblk - 1) / nblk;
+  int b, cb;
+  xcd_block<true>(b, cb);
+  const int t_end = min(total, b * per + per), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto coords = [&](int t, int& n, int& oy, int& ox) {
+    const int tx = t % tiles_x, r = t / tiles_x;
+    oy = r % p.Hout;
+    n = r / p.Hout;
+    ox = tx * 32 + (threadIdx.x & 31);
+  };
+  int t = b * per + wave;
+  if (t >= t_end) return;   // wave-uniform; no barrier follows
+  f32x4 q[RGB5_KY][3];
+  {
+    int n, oy, ox;
+    coords(t, n, oy, ox);
+    rgb5_load(p, n, oy, ox, ox < p.Wout, q);
+  }
+#pragma unroll 1
+  for (; t < t_end; t += 4) {
+    int n, oy, ox;
+    coords(t, n, oy, ox);
+    const bool valid = ox < p.Wout;
+    f32x4 yq[RGB5_IT][4], sq[RGB5_IT][4];
+    gdn_bwd_x6_load<RGB5_IT>(p, n, oy, ox, valid, yq, sq);
+    f32x16 acc[RGB5_IT];
+#pragma unroll
+    for (int it = 0; it < RGB5_IT; ++it) acc[it] = f32x16{0};
+    rgb5_main(rgb5_lds, q, acc);
+    if (t + 4 < t_end) {
+      int n1, oy1, ox1;
+      coords(t + 4, n1, oy1, ox1);
+      rgb5_load(p, n1, oy1, ox1, ox1 < p.Wout, q);
+    }
+    rgb5_epi_bwd<EPI>(p, rgb5_lds, acc, n, oy, ox, valid, yq, sq);
   }
 }
 
@@ -1646,6 +1786,38 @@ __global__ void pack_conv_x6w_kernel(const float* __restrict__ w, __bf16* __rest
   dst[2 * total + i] = (__bf16)(r1 - (float)b);
 }
 
+// dense tap-row fragments of conv_rgb5_x6, [cb][ky][it][lane][e] (three split planes): lane (h, r) supplies
+// A[r][k = 8 h + e] = W[o][c][ky][kx] with (kx, c) of the conv_rgb5_x6 K map (0 for c >= C and for h = 1, e = 7)
+__global__ void pack_conv_rgb5_x6_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int O, int C, long so,
+                                         long sc, int IT, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  long t = i;
+  const int e = t % 8; t /= 8;
+  const int lane = t % 64; t /= 64;
+  const int it = t % IT; t /= IT;
+  const int ky = t % RGB5_KY;
+  const int cb = (int)(t / RGB5_KY);
+  const int h = lane >> 5;
+  int kx, c;
+  if (e < 6) {
+    kx = 2 * h + e / 3;
+    c = e % 3;
+  } else {
+    kx = 4;
+    c = h ? (e == 6 ? 2 : 3) : e - 6;   // c = 3: the zero slot
+  }
+  const int o = cb * IT * 32 + it * 32 + (lane & 31);
+  float v = 0.f;
+  if (o < O && c < C && c < 3) v = w[o * so + c * sc + ky * 5 + kx];
+  const __bf16 a = (__bf16)v;
+  const float r1 = v - (float)a;
+  const __bf16 b = (__bf16)r1;
+  dst[i] = a;
+  dst[total + i] = b;
+  dst[2 * total + i] = (__bf16)(r1 - (float)b);
+}
+
 // the fp32 gamma' pack of ica_pack_gdn ([a][b][lane][r]) -> three bf16 planes [plane][a][b][s][lane][e], r = 8s + e
 // (the epilogue's k-step s of tile b, lane order unchanged)
 __global__ void pack_gdn_x6_kernel(const float* __restrict__ gp, __bf16* __restrict__ dst, long total) {
@@ -1876,19 +2048,27 @@ int launch_down_x6(const ConvParams& p, hipStream_t st) {
   return launch_down_x6_pt<IT, EPI, X6_PT>(p, st);
 }
 
-template <int IT, int EPI>
+static inline long rgb5_plane_frags(int O, int IT) { return (long)((O + IT * 32 - 1) / (IT * 32)) * RGB5_KY * IT * 64; }
+
+template <int EPI>
 int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
-  const int tiles = ((p.Wout + 31) / 32) * ((p.Hout + 3) / 4) * p.N;
-  const int ncb = (p.Cout + IT * 32 - 1) / (IT * 32);
-  const long ps = (long)ncb * 9 * IT * 64;
-  if constexpr (EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD) {
-    // one block per CU, a contiguous run of tiles each (the XCD-aware order keeps a run's halo rows in one L2)
-    const int nblk = std::max(1, std::min(tiles, ica_cu_count() / ncb));
-    const int per = (tiles + nblk - 1) / nblk;
-    ICA_LAUNCH((conv_rgb_bwd_x6_kernel<IT, EPI>), dim3((tiles + per - 1) / per, ncb), dim3(256), 0, st, p, ps,
-                       per);
+  if (p.Cout != 32 * RGB5_IT) return -3;   // the LDS-resident weights: one 128-row block
+  const long ps = rgb5_plane_frags(p.Cout, RGB5_IT);
+  const int total = ((p.Wout + 31) / 32) * p.Hout * p.N;
+  constexpr bool BWD = EPI == EPI_IGDN_BWD || EPI == EPI_GDN_BWD;
+  // one persistent block per CU; its waves take consecutive row tiles of a contiguous run
+  const int nblk = std::max(1, std::min(ica_cu_count(), (total + (BWD ? 3 : 7)) / (BWD ? 4 : 8)));
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(BWD ? reinterpret_cast<const void*>(&conv_rgb5_bwd_x6_kernel<BWD ? EPI : EPI_IGDN_BWD>)
+                                  : reinterpret_cast<const void*>(&conv_rgb5_x6_kernel<BWD ? EPI_GDN : EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RGB5_LDS);
+    attr_set = true;
+  }
+  if constexpr (BWD) {
+    ICA_LAUNCH((conv_rgb5_bwd_x6_kernel<EPI>), dim3(nblk), dim3(256), RGB5_LDS, st, p, ps, nblk);
   } else {
-    ICA_LAUNCH((conv_rgb_x6_kernel<IT, EPI>), dim3(tiles, ncb), dim3(256), 0, st, p, ps);
+    ICA_LAUNCH((conv_rgb5_x6_kernel<EPI>), dim3(nblk), dim3(512), RGB5_LDS, st, p, ps, nblk);
   }
   ICA_CHECK_LAUNCH();
   return 0;
@@ -2057,13 +2237,13 @@ int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, i
   if (p.Cout % 32 != 0) return -4;
   if (kind == 0) {
     if (p.Hout * 2 != p.Hin + (p.Hin & 1) || p.Wout * 2 != p.Win + (p.Win & 1)) return -2;
-    if (p.Cin <= 4) {   // RGB-sized input: the PixelUnshuffle(2) k3 view (wp from the rearranged weight)
-      if (it != 4) return -3;
+    if (p.Cin <= 4) {   // RGB-sized input: conv_rgb5_x6 on the dense tap-row pack (ica_pack_conv_weight_x6 order 2)
+      if (it != 4 || p.Cin > 3) return -3;
       if (p.pl & PL_IN) return -2;   // the image side stays row-major
       switch (epi) {
-        case EPI_BIAS: return launch_rgb_x6<4, EPI_BIAS>(p, st);
-        case EPI_GDN: return launch_rgb_x6<4, EPI_GDN>(p, st);
-        case EPI_IGDN_BWD: return launch_rgb_x6<4, EPI_IGDN_BWD>(p, st);
+        case EPI_BIAS: return launch_rgb_x6<EPI_BIAS>(p, st);
+        case EPI_GDN: return launch_rgb_x6<EPI_GDN>(p, st);
+        case EPI_IGDN_BWD: return launch_rgb_x6<EPI_IGDN_BWD>(p, st);
         default: return -5;
       }
     }
@@ -2114,10 +2294,20 @@ int ica_pack_gdn_x6(const float* gp, void* dst, int C, hipStream_t st) {
 }
 
 // three bf16 planes (hi, mid, lo) of the 16-channel-chunk fragment pack; order 0: conv_down [cb][chunk][tap],
-// order 1: conv_up [cb][tap][chunk]
+// order 1: conv_up [cb][tap][chunk]; order 2: the dense tap-row pack of a k5 conv_down with C <= 3 input channels
+// (conv_rgb5_x6: g_a.0 forward, g_s.6 input gradient), [cb][ky][it] (smaller than the size above)
 int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
                             hipStream_t st) {
   if (it <= 0) return -3;
+  if (order == 2) {
+    if (KS != 5 || C > 3 || C <= 0) return -2;
+    const long t3 = rgb5_plane_frags(O, it) * 8;
+    ICA_LAUNCH(pack_conv_rgb5_x6_kernel, dim3((t3 + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
+               O, C, so, sc, it, t3);
+    ICA_CHECK_LAUNCH();
+    return 0;
+  }
+  if (order != 0 && order != 1) return -2;
   const long total = x6_plane_frags(O, C, KS, it) * 8;
   ICA_LAUNCH(pack_conv_x6_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w,
                      reinterpret_cast<__bf16*>(dst), O, C, KS, so, sc, it, order, total);

@@ -20,6 +20,22 @@ import torch
 import torch.distributed as dist
 
 
+# Optional timing hook (bench.py --config 4): {"grad": [(ev0, ev1), ...], "couple": [...]}, HIP events recorded on the
+# issuing stream around each collective of the fine-tune (no synchronisation)
+COLL_HOOK = None
+
+
+def _timed(kind, fn):
+    if COLL_HOOK is None or not torch.cuda.is_available():
+        return fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    r = fn()
+    e1.record()
+    COLL_HOOK.setdefault(kind, []).append((e0, e1))
+    return r
+
+
 def env_world():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), \
         int(os.environ.get("LOCAL_RANK", "0"))
@@ -57,10 +73,10 @@ def allreduce_mean_(t: torch.Tensor, group=None, world: int | None = None) -> to
     return t
 
 
-def allreduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
-    """In-place sum over ranks (one collective for the whole buffer)."""
+def allreduce_sum_(t: torch.Tensor, group=None, kind: str = "grad") -> torch.Tensor:
+    """In-place sum over ranks (one collective for the whole buffer); `kind` names it in COLL_HOOK."""
     if group is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        _timed(kind, lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group))
     return t
 
 
@@ -69,7 +85,7 @@ def couple_loss_i(loss_i: torch.Tensor, B_global: int, group=None) -> torch.Tens
     becomes the mean over the global batch (attack_rd.py:333 applied to the whole batch)."""
     tot = loss_i.sum().reshape(1)
     if group is not None:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)
+        _timed("couple", lambda: dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group))
     loss_i.copy_((tot / B_global).expand(loss_i.shape[0]))
     return loss_i
 

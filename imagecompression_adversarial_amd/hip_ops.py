@@ -15,6 +15,7 @@ from ._lib import ConvArgs, call, lib, ptr, stream
 EPI_BIAS, EPI_RELU, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD, EPI_LRELU, EPI_LRELU_BWD = range(8)
 FILL_PLAIN, FILL_LRELU_MASK, FILL_UNSHUFFLE = range(3)
 ORDER_DOWN, ORDER_UP = 0, 1
+ORDER_RGB5 = 2   # ica_pack_conv_weight_x6: dense tap-row pack of a k5 conv_down with <= 3 input channels
 # parity-split tensors of an x6 k5 s2 launch (ica_conv_args.layout): the input x, the output-layout tensors
 LAYOUT_IN, LAYOUT_OUT = 1, 2
 GDN_BETA_BOUND = float((1e-6 + 2.0 ** -36) ** 0.5)  # NonNegativeParametrizer bound (utils/ops.py:67)
@@ -202,16 +203,6 @@ def pack_conv_x6(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, or
     return dst
 
 
-def rgb_unshuffle_weight(w: torch.Tensor) -> torch.Tensor:
-    """k5 s2 weight [O][C <= 4][5][5] of a conv whose input is an RGB-sized map -> the k3 weight [O][16][3][3] of
-    its PixelUnshuffle(2) view (conv_rgb_x6_kernel): w'[o][4 (2 sy + sx) + c][ty][tx] = w[o][c][2 ty + sy][2 tx + sx],
-    zero where a tap index reaches 5."""
-    O, C = w.shape[0], w.shape[1]
-    wp = torch.zeros(O, 4, 6, 6, dtype=w.dtype, device=w.device)
-    wp[:, :C, :5, :5] = w.detach()
-    return wp.view(O, 4, 3, 2, 3, 2).permute(0, 3, 5, 1, 2, 4).reshape(O, 16, 3, 3).contiguous()
-
-
 def x6_ok(O: int, C: int, it: int, kind: int) -> bool:
     """Shapes ica_conv_x6_dispatch (ica_conv_x6.hip) covers for a k5 s2 launch with O output / C input channels:
     kind 0 (conv_down): C >= 16, a multiple of 16; O = 128-multiples (IT 4: bias, GDN, IGDN_BWD) or 96-multiples
@@ -319,15 +310,15 @@ class PackedConv:
 
     def _init_x6(self, weight, bias, kind, stride):
         """PREC_X6: the k5 s2 launches run on the bf16x6 kernels: >= 16 channels on both ends (conv_down_x6 /
-        conv_up_x6) and the conv_downs whose input is RGB-sized (g_a.0 forward, g_s.6 input gradient: conv_rgb_x6 on
-        the PixelUnshuffle(2) view) and the 3-channel transposed-conv outputs (x6 conv_up3).  Explicit 6-tile layers
+        conv_up_x6) and the conv_downs whose input has <= 3 channels (g_a.0 forward, g_s.6 input gradient: conv_rgb5_x6
+        with the 75 (tap, channel) pairs packed densely into 5 K steps) and the 3-channel transposed-conv outputs (x6 conv_up3).  Explicit 6-tile layers
         keep the fp32 packs."""
         fp = PackedConv(weight, bias, kind, stride, PREC_FP32, self.it_fwd, self.it_bwd)
         self.__dict__.update(fp.__dict__)
         if self.KS != 5 or stride != 2:
             return
         KK = 25
-        rgb_ok = lambda O, it: it == 0 and x6_it(O) == 4   # noqa: E731  (conv_rgb_x6: IT 4 launches)
+        rgb_ok = lambda O, C, it: it == 0 and C <= 3 and O == 128   # noqa: E731  (conv_rgb5_x6: one 128-row block)
         if kind == "conv" and self.Cin == 3 and self.Cout % 16 == 0:    # input gradient to RGB: x6 conv_up3
             self.bwd = pack_up3(weight, PREC_X6)
             self.bwd_prec = PREC_X6
@@ -335,8 +326,8 @@ class PackedConv:
             self.fwd = pack_up3(weight, PREC_X6)
             self.fwd_prec = PREC_X6
         if kind == "conv":
-            if self.Cin <= 4 and rgb_ok(self.Cout, self.it_fwd):   # forward from the RGB image: unshuffled k3 view
-                self.fwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cout, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
+            if rgb_ok(self.Cout, self.Cin, self.it_fwd):   # forward from the RGB image: dense tap-row K
+                self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_RGB5, 4)
                 self.fwd_prec = PREC_X6
             elif x6_ok(self.Cout, self.Cin, self.it_fwd, 0):  # forward conv_down: o = co, c = ci
                 self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN, x6_it(self.Cout))
@@ -348,8 +339,8 @@ class PackedConv:
             if self.Cout != 3 and x6_ok(self.Cout, self.Cin, self.it_fwd, 1):  # forward conv_up: o = co, c = ci
                 self.fwd = pack_conv_x6(weight, self.Cout, self.Cin, 5, KK, self.Cout * KK, ORDER_UP, x6_it(self.Cout))
                 self.fwd_prec = PREC_X6
-            if self.Cout <= 4 and rgb_ok(self.Cin, self.it_bwd):   # dgrad from the RGB-sized gradient (view [ci][co])
-                self.bwd = pack_conv_x6(rgb_unshuffle_weight(weight), self.Cin, 16, 3, 16 * 9, 9, ORDER_DOWN, 4)
+            if rgb_ok(self.Cin, self.Cout, self.it_bwd):   # dgrad from the RGB-sized gradient (view [ci][co])
+                self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_RGB5, 4)
                 self.bwd_prec = PREC_X6
             elif x6_ok(self.Cin, self.Cout, self.it_bwd, 0):    # dgrad conv_down: o = ci, c = co
                 self.bwd = pack_conv_x6(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, x6_it(self.Cin))

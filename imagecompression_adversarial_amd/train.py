@@ -112,7 +112,7 @@ def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, g
         keys = ("loss", "bpp_loss", "distortion_loss")
         vals = torch.stack([torch.as_tensor(out[k], device=batch_x.device, dtype=torch.float32).reshape(())
                             for k in keys]) * w
-        D.allreduce_sum_(vals, group)
+        D.allreduce_sum_(vals, group, kind="loss")
         out.update({k: vals[i] for i, k in enumerate(keys)})
     torch.nn.utils.clip_grad_norm_(main_parameters(net), 1.0)
     optimizer.step()

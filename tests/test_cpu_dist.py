@@ -51,6 +51,10 @@ def _worker(rank, world, port, q):
             torch.nn.utils.clip_grad_norm_(params, 1.0)
             opt.step()
         out["params"] = torch.cat([p.detach().flatten() for p in params]).tolist()
+        # 4. the N > 1 bench line's per-rank evidence (bench._rank_stats): gathered before the MAX
+        import bench
+        out["ranks"] = bench._rank_stats(dist, torch.device("cpu"), 1.0 + rank, 10.0 * (rank + 1), w,
+                                         extra=0.25 * rank)
         q.put((rank, out))
     except Exception as e:  # surface failures to the parent
         q.put((rank, {"error": repr(e)}))
@@ -79,6 +83,19 @@ def test_gloo_world2():
     for r in (0, 1):
         assert all(abs(v - mean) < 1e-10 for v in res[r]["loss_i"])
     assert res[0]["params"] == res[1]["params"]
+    rk = res[0]["ranks"]
+    assert rk == res[1]["ranks"]
+    assert rk["backend"] == "gloo" and rk["world_size"] == 2
+    assert rk["rank_elapsed_s"] == [1.0, 2.0] and rk["rank_value"] == [10.0, 10.0]
+    assert rk["elapsed_min_s"] == 1.0 and rk["elapsed_max_s"] == 2.0 and rk["imbalance"] == 1.0
+    assert rk["rank_extra"] == [0.0, 0.25] and rk["rank_device"] == [-1, -1]
+
+
+def test_rank_stats_single_process():
+    import bench
+    rk = bench._rank_stats(None, torch.device("cpu"), 2.0, 64.0, 1)
+    assert rk["backend"] is None and rk["world_size"] == 1
+    assert rk["rank_value"] == [32.0] and rk["imbalance"] == 0.0
 
 
 @pytest.mark.parametrize("n,world", [(32, 8), (5, 2), (7, 3), (1, 4)])
