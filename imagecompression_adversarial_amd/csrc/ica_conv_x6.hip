@@ -573,6 +573,18 @@ __global__ __launch_bounds__(512, 1) void conv_down_x6w_kernel(ConvParams p, lon
 // Weights: [plane][ky][it][lane][e] (pack_conv_rgb5_x6_kernel, ica_pack_conv_weight_x6 order 2), plane stride ps.
 // --------------------------------------------------------------------------------------------------------------
 constexpr int RGB5_KY = 5, RGB5_IT = 4;
+#ifndef RGB5_STAGGER
+#define RGB5_STAGGER 0
+#endif
+#ifndef RGB5_PRIO
+#define RGB5_PRIO 0
+#endif
+#ifndef RGB5_W
+#define RGB5_W 0    // 1: the GDN / IGDN forward on the one-wave-per-SIMD kernel (conv_rgb5w_x6_kernel)
+#endif
+#ifndef RGB5_BJ
+#define RGB5_BJ 1   // 1: the backward epilogue's gamma'^T fragments one MFMA group ahead
+#endif
 #ifndef RGB5_AB
 #define RGB5_AB 0   // timing-only A/B builds (scripts/build_variant.sh): 1 = 1/16 of the forward stores, 2 = no GDN GEMM
 #endif
@@ -712,7 +724,7 @@ ICA_DEV void rgb5_epi_fwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RG
         for (int e = 0; e < 4; ++e) nx[4 * g + e] = ev[e];
       }
       bf16x8 ga[2][3];
-#if RGB5_AB != 2
+#if RGB5_AB != 2 && RGB5_AB != 3
       ldg(ga[0], ct, 0);
 #pragma unroll
       for (int k = 0; k < 2 * IT; ++k) {
@@ -746,6 +758,76 @@ ICA_DEV void rgb5_epi_fwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RG
         }
       }
     }
+  }
+}
+
+// the same epilogue at one wave per SIMD (512 registers): every normaliser tile at once (4 accumulation chains), x^2
+// split one k-step at a time (the round's 8 values feed all 4 output tiles), gamma' fragments from LDS one output
+// tile ahead; the ops of the narrow form, the MFMA order of gdn_fwd_x6_pair
+template <int EPI>
+ICA_DEV void rgb5_epi_fwd_wide(const ConvParams& p, const char* lds, f32x16 (&acc)[RGB5_IT], int n, int oy, int ox,
+                               bool valid) {
+  constexpr int IT = RGB5_IT;
+  static_assert(EPI == EPI_GDN || EPI == EPI_IGDN, "forward GDN epilogues");
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const unsigned plane = (unsigned)p.Hout * p.Wout;
+  const size_t img = (size_t)((p.Cout + 3) >> 2) * plane;
+  const Img4 Y(p.y, img, n), SS(p.save_s, img, n);
+  const f32x4* bq = reinterpret_cast<const f32x4*>(lds + RGB5_W_BYTES + RGB5_G_BYTES);   // [32 bias][32 beta'] quads
+  const unsigned vo = h * plane + (valid ? pix_at(oy, ox, p.Hout, p.Wout, p.pl & PL_OUT) : 0u);
+  const char* gl = lds + RGB5_W_BYTES;
+  f32x16 nx[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = bq[it * 8 + 2 * g + h], ev = bq[32 + it * 8 + 2 * g + h];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[it][4 * g + e] += bv[e];
+        nx[it][4 * g + e] = ev[e];
+      }
+    }
+  auto ldg = [&](bf16x8 (&a)[3], int ct, int k) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      a[pl] = lds_frag(gl, (((ct * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + pl * IT * IT * 2048 + lane * 16);
+  };
+  bf16x8 ga[2][3];
+  ldg(ga[0], 0, 0);
+#pragma unroll
+  for (int k = 0; k < 2 * IT; ++k) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = acc[k >> 1][8 * (k & 1) + j] * acc[k >> 1][8 * (k & 1) + j];
+    bf16x8 xq[3];
+    split3x8(v, xq);
+#pragma unroll
+    for (int ct = 0; ct < IT; ++ct) {
+      const int r = k * IT + ct;
+      if (r + 1 < 2 * IT * IT) ldg(ga[(r + 1) & 1], (r + 1) % IT, (r + 1) / IT);
+      __builtin_amdgcn_sched_barrier(0);
+      nx[ct] = mfma_x6(ga[r & 1], xq, nx[ct]);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (valid) {
+#pragma unroll
+    for (int ct = 0; ct < IT; ++ct)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 yv, sv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float nv = nx[ct][4 * g + e];
+          const float sc = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+          sv[e] = sc;
+          yv[e] = acc[ct][4 * g + e] * sc;
+        }
+        const unsigned ss = (unsigned)(ct * 8 + 2 * g) * plane;
+        if (p.save_s) SS.st(vo, ss, sv);
+        Y.st(vo, ss, yv);
+      }
   }
 }
 
@@ -785,6 +867,25 @@ ICA_DEV void rgb5_epi_bwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RG
   f32x16 ux[IT];
 #pragma unroll
   for (int jt = 0; jt < IT; ++jt) ux[jt] = f32x16{0};
+  __builtin_amdgcn_sched_barrier(0);
+#if RGB5_BJ
+  // fragments one MFMA group (k, jt) ahead: 24 registers instead of two rounds' 96
+  bf16x8 ga[2][3];
+  auto ldg = [&](bf16x8 (&a)[3], int r) {
+    const int k = r / IT, jt = r % IT;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      a[pl] = lds_frag(gl, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + pl * IT * IT * 2048 + lane * 16);
+  };
+  ldg(ga[0], 0);
+#pragma unroll
+  for (int r = 0; r < 2 * IT * IT; ++r) {
+    if (r + 1 < 2 * IT * IT) ldg(ga[(r + 1) & 1], r + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const int k = r / IT, jt = r % IT;
+    ux[jt] = mfma_x6(ga[r & 1], tq[k >> 1][k & 1], ux[jt]);
+  }
+#else
   bf16x8 ga[2][IT][3];
   auto ldg = [&](bf16x8 (&a)[IT][3], int k) {
 #pragma unroll
@@ -793,7 +894,6 @@ ICA_DEV void rgb5_epi_bwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RG
       for (int pl = 0; pl < 3; ++pl)
         a[jt][pl] = lds_frag(gl, (((jt * IT + (k >> 1)) * 2 + (k & 1)) * 1024) + pl * IT * IT * 2048 + lane * 16);
   };
-  __builtin_amdgcn_sched_barrier(0);
   ldg(ga[0], 0);
 #pragma unroll
   for (int k = 0; k < 2 * IT; ++k) {
@@ -802,6 +902,7 @@ ICA_DEV void rgb5_epi_bwd(const ConvParams& p, const char* lds, f32x16 (&acc)[RG
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt) ux[jt] = mfma_x6(ga[k & 1][jt], tq[k >> 1][k & 1], ux[jt]);
   }
+#endif
   if (valid) {
 #pragma unroll
     for (int jt = 0; jt < IT; ++jt)
@@ -826,6 +927,17 @@ __global__ __launch_bounds__(512, 1) void conv_rgb5_x6_kernel(ConvParams p, long
   int b, cb;
   xcd_block<true>(b, cb);
   const int t_end = min(total, b * per + per), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if RGB5_STAGGER > 0
+  // the SIMD partners (waves w, w + 4) run the same tile program and would stay in lockstep, both in their MFMA
+  // phase, then both in their store phase; waves 4-7 start RGB5_STAGGER x 4096 cycles late
+  if (wave >= 4) {
+#pragma unroll 1
+    for (int i = 0; i < RGB5_STAGGER; ++i) __builtin_amdgcn_s_sleep(64);
+  }
+#endif
+#if RGB5_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll 1
   for (int t = b * per + wave; t < t_end; t += 8) {
     const int tx = t % tiles_x, r = t / tiles_x;
@@ -836,8 +948,57 @@ __global__ __launch_bounds__(512, 1) void conv_rgb5_x6_kernel(ConvParams p, long
     f32x16 acc[RGB5_IT];
 #pragma unroll
     for (int it = 0; it < RGB5_IT; ++it) acc[it] = f32x16{0};
+#if RGB5_AB == 3
+#pragma unroll
+    for (int it = 0; it < RGB5_IT; ++it) acc[it] = f32x16{q[it][0][0] + q[4][1][1]};
+#else
     rgb5_main(rgb5_lds, q, acc);
+#endif
     rgb5_epi_fwd<EPI>(p, rgb5_lds, acc, n, oy, ox, valid);
+  }
+}
+
+// GDN / IGDN forward at one wave per SIMD: tile i+1's input quads are issued before tile i's epilogue, so the wait
+// for them does not include tile i's stores (vmcnt counts loads and stores together, in order: loaded after the
+// stores, every tile start waited for the previous tile's stores to complete, and the stores never overlapped the
+// MFMAs)
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void conv_rgb5w_x6_kernel(ConvParams p, long ps, int nblk) {
+  extern __shared__ __attribute__((aligned(16))) char rgb5_lds[];
+  rgb5_stage<true>(p, ps, rgb5_lds);
+  const int tiles_x = (p.Wout + 31) / 32, total = tiles_x * p.Hout * p.N, per = (total + nblk - 1) / nblk;
+  int b, cb;
+  xcd_block<true>(b, cb);
+  const int t_end = min(total, b * per + per), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto coords = [&](int t, int& n, int& oy, int& ox) {
+    const int tx = t % tiles_x, r = t / tiles_x;
+    oy = r % p.Hout;
+    n = r / p.Hout;
+    ox = tx * 32 + (threadIdx.x & 31);
+  };
+  int t = b * per + wave;
+  if (t >= t_end) return;   // wave-uniform; no barrier follows
+  f32x4 q[RGB5_KY][3];
+  {
+    int n, oy, ox;
+    coords(t, n, oy, ox);
+    rgb5_load(p, n, oy, ox, ox < p.Wout, q);
+  }
+#pragma unroll 1
+  for (; t < t_end; t += 4) {
+    int n, oy, ox;
+    coords(t, n, oy, ox);
+    const bool valid = ox < p.Wout;
+    f32x16 acc[RGB5_IT];
+#pragma unroll
+    for (int it = 0; it < RGB5_IT; ++it) acc[it] = f32x16{0};
+    rgb5_main(rgb5_lds, q, acc);
+    if (t + 4 < t_end) {
+      int n1, oy1, ox1;
+      coords(t + 4, n1, oy1, ox1);
+      rgb5_load(p, n1, oy1, ox1, ox1 < p.Wout, q);
+    }
+    rgb5_epi_fwd_wide<EPI>(p, rgb5_lds, acc, n, oy, ox, valid);
   }
 }
 
@@ -2067,6 +2228,15 @@ int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
   }
   if constexpr (BWD) {
     ICA_LAUNCH((conv_rgb5_bwd_x6_kernel<EPI>), dim3(nblk), dim3(256), RGB5_LDS, st, p, ps, nblk);
+  } else if constexpr (RGB5_W && EPI != EPI_BIAS) {
+    const int nb4 = std::max(1, std::min(ica_cu_count(), (total + 3) / 4));
+    static bool attr_w = false;
+    if (!attr_w) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_rgb5w_x6_kernel<EPI>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, RGB5_LDS);
+      attr_w = true;
+    }
+    ICA_LAUNCH((conv_rgb5w_x6_kernel<EPI>), dim3(nb4), dim3(256), RGB5_LDS, st, p, ps, nb4);
   } else {
     ICA_LAUNCH((conv_rgb5_x6_kernel<EPI>), dim3(nblk), dim3(512), RGB5_LDS, st, p, ps, nblk);
   }
