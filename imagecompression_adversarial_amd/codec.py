@@ -411,6 +411,7 @@ class MaskedConv2d(nn.Conv2d):
     def forward(self, x):
         if self.mask_type != "A":
             raise NotImplementedError("mask type B is not used by cheng2020 / mbt2018")
+        self.weight.data *= self.mask   # as CompressAI's forward: the stored weight keeps its masked taps at zero
         k = (self.weight.data_ptr(), self.weight._version, self.bias.data_ptr(), self.bias._version)
         if self._ex is None or self._ex_key != k:
             self._ex = EC.ChengContext({"weight": self.weight.detach(), "bias": self.bias.detach()}, prefix="")

@@ -2297,25 +2297,24 @@ int launch_up_x6(const ConvParams& p, hipStream_t st) {
   const long b2 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<2>() - 1) / xu_th<2>()) * p.N * ncb;
   const long b1 = (long)((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<1>() - 1) / xu_th<1>()) * p.N * ncb;
   constexpr bool BWD = EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD;
-  if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) {
-#ifndef ICA_UP_BWD4
-    // the GDN backward's 8-wave kernel at PT = 1: the same bits as its PT = 2 form (a batch and its images alone
-    // may take different PT)
-    if constexpr (IT == 4 && BWD) return launch_up_x6w<IT, EPI, CG, 1>(p, st);
+  // The GDN backward: the 4-wave kernel (one (y, s) read per output, its wide epilogue) for 128-channel inputs, the
+  // 8-wave slab kernel for 64-channel groups (Cin = 192: g_a.6's input gradient).  At config 2 the 8-wave slab kernel
+  // of round 5 took g_a.2.dgrad 3.56 -> 3.63-3.67 ms and 5.83 -> 8.84 GB per launch ((y, s) read twice at PT = 2);
+  // for the 32 x 48-input g_a.6.dgrad it is the faster one (0.335 vs 0.41 ms).  PT follows the round fill; each
+  // family's PT = 1 and PT = 2 forms give the same bits, and the family depends on the layer only (batch-independent
+  // bits).  ICA_UPW_BWD_ALL builds put every GDN backward on the slab kernel (round 5) for A/B runs.
+#ifdef ICA_UPW_BWD_ALL
+  constexpr bool SLAB = BWD && IT == 4;
+#else
+  constexpr bool SLAB = BWD && IT == 4 && CG == 64;
 #endif
+  if (x6_round_fill(b1) > x6_round_fill(b2) + 0.15) {
+    if constexpr (SLAB) return launch_up_x6w<IT, EPI, CG, 1>(p, st);
     return launch_up_x6_pt<IT, EPI, CG, 1>(p, st);
   }
-  // the 8-wave class-per-wave kernel: forward layers (bias / IGDN) and, since round 5, the GDN backward with t in LDS
-  // slabs (gdn_bwd_x6w_slab; ICA_UP_BWD4 builds keep the 4-wave kernel's wide epilogue for A/B runs)
-#ifndef ICA_UPW_BWD_PT
-#define ICA_UPW_BWD_PT 2
-#endif
-#ifdef ICA_UP_BWD4
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_IGDN || EPI == EPI_GDN) return launch_up_x6w<IT, EPI, CG>(p, st);
-#else
-  if constexpr (IT == 4 && BWD) return launch_up_x6w<IT, EPI, CG, ICA_UPW_BWD_PT>(p, st);
-  if constexpr (IT == 4) return launch_up_x6w<IT, EPI, CG>(p, st);
-#endif
+  // the 8-wave class-per-wave kernel: forward layers (bias / IGDN) and the slab GDN backward
+  if constexpr (SLAB) return launch_up_x6w<IT, EPI, CG, 2>(p, st);
+  if constexpr (IT == 4 && !BWD) return launch_up_x6w<IT, EPI, CG>(p, st);
   return launch_up_x6_pt<IT, EPI, CG, X6_PT>(p, st);
 }
 

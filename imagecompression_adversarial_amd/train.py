@@ -114,7 +114,7 @@ def adv_step(net, trainer: RDTrainer, optimizer, aux_optimizer, batch_x, args, g
                             for k in keys]) * w
         D.allreduce_sum_(vals, group, kind="loss")
         out.update({k: vals[i] for i, k in enumerate(keys)})
-    torch.nn.utils.clip_grad_norm_(main_parameters(net), 1.0)
+    out["grad_norm"] = torch.nn.utils.clip_grad_norm_(main_parameters(net), 1.0).detach()
     optimizer.step()
     aux_loss = net.aux_loss()
     aux_loss.backward()

@@ -16,7 +16,8 @@ oracle's restatement is ``oracle/codec.cheng_forward``):
 
 Weight gradients are ``ica_wgrad`` GEMMs over pixels (k3 s1 / k3 s2 / k1 s2 / k1 s1 / k5 s1); the subpel convs
 (rho-ordered rows, ``engine_cheng._rho_weight``) take theirs from the PixelUnshuffle view of the output gradient and
-scatter the rows back to CompressAI order; the masked conv's gradient is masked like its weight in the forward
+scatter the rows back to CompressAI order; the masked conv's gradient is its full 5x5 weight gradient (CompressAI
+applies the mask to weight.data, outside autograd)
 (``oracle/codec.context_prediction``). GDN / IGDN parameter gradients come from t = dL/dn (``ica_gdn_t``) of the
 summed gradient the fused GDN backward saves, then the NonNegativeParametrizer chain (``train_engine
 .gdn_param_grads``). All operands fp32 (the inner attack runs on the model's attack precision)."""
@@ -45,12 +46,25 @@ def _conv(P, pre, stride=1, mask=None):
 
 def entropy_forward(P, y4, M, params4, noise_y=None):
     """The joint entropy model in train mode (cheng2020 and mbt2018, anchors/model.py:97-106): y_hat = y + u, the
-    masked context model, entropy_parameters(cat(h_s params, ctx)) -> (scales, means), GaussianConditional."""
+    masked context model, entropy_parameters(cat(h_s params, ctx)) -> (scales, means), GaussianConditional.
+    noise_y: None draws CompressAI's two independent U(-1/2, 1/2) tensors (y_hat = quantize(y, "noise") and the
+    GaussianConditional's own requantisation of y); a pair (y_hat noise, likelihood noise) pins both; one tensor pins
+    a draw shared by both (tests).  The masked conv zeroes its masked taps in the parameter itself, as CompressAI's
+    MaskedConv2d.forward does (``weight.data *= mask``)."""
     B = y4.shape[0]
-    if noise_y is None:
-        noise_y = torch.empty((B, M, y4.shape[2], y4.shape[3]), device=y4.device).uniform_(-0.5, 0.5)
-    ny4 = K.to_nc4(noise_y.contiguous())
+    shape = (B, M, y4.shape[2], y4.shape[3])
+    if isinstance(noise_y, (tuple, list)):
+        n_hat, n_lik = noise_y
+    elif noise_y is None:
+        n_hat = torch.empty(shape, device=y4.device).uniform_(-0.5, 0.5)
+        n_lik = torch.empty(shape, device=y4.device).uniform_(-0.5, 0.5)
+    else:
+        n_hat = n_lik = noise_y
+    ny4 = K.to_nc4(n_hat.contiguous())
+    nl4 = ny4 if n_lik is n_hat else K.to_nc4(n_lik.contiguous())
     yh4 = y4 + ny4                                     # y_hat = quantize(y, "noise") (train mode)
+    wctx = P("context_prediction.weight")
+    wctx.mul_(context_mask(5).to(wctx.device))         # MaskedConv2d: weight.data *= mask (in place)
     ctxc = _conv(P, "context_prediction", mask=context_mask(5))
     ctx4 = ctxc.forward(yh4, K.EPI_BIAS)
     ep = [_conv(P, f"entropy_parameters.{i}") for i in (0, 2, 4)]
@@ -60,7 +74,7 @@ def entropy_forward(P, y4, M, params4, noise_y=None):
     gp4 = ep[2].forward(e1, K.EPI_BIAS)
     c4 = (M + 3) // 4
     scales4, means4 = gp4[:, :c4].contiguous(), gp4[:, c4:].contiguous()
-    yt4, ylik4, _ = K.gc_likelihood(y4, M, scales4, means4, True, ny4)
+    yt4, ylik4, _ = K.gc_likelihood(y4, M, scales4, means4, True, nl4)
     return {"yh4": yh4, "ctxc": ctxc, "ep": ep, "t0": t0, "e0": e0, "e1": e1, "scales4": scales4,
             "means4": means4, "yt4": yt4, "ylik4": ylik4}
 
@@ -162,7 +176,8 @@ class ChengTrainStep:
         g = ep[0].dgrad(g)
         cp = params4.shape[1]
         gparams, gctx = g[:, :cp].contiguous(), g[:, cp:].contiguous()
-        self._wb(gctx, 2 * M, yh4, M, 5, 1, "context_prediction", mask=context_mask(5))
+        # CompressAI masks the weight outside autograd: its gradient is the full 5x5 conv gradient
+        self._wb(gctx, 2 * M, yh4, M, 5, 1, "context_prediction")
         gy.add_(ctxc.dgrad(gctx))
         return gparams
 

@@ -284,32 +284,40 @@ def rd_loss(out, target, metric="mse", lmbda=0.0067):
 
 def adv_train_step(P, batch_x, steps=300, noise_thr=1e-4, epsilon=16.0, lr_attack=0.01, att_metric="L2",
                    clamp=True, model="hyper", metric="mse", lmbda=0.0130, lr_train=1e-4, noise_y=None,
-                   noise_z=None, record=None):
+                   noise_z=None, record=None, state=None):
     """One outer step of train.py --adv (train.py:335-366): the batch-coupled inner attack (attack_rd.attack_
     on the whole batch, train.py:342), the train-mode forward of the adversarial batch with the given
     quantisation noise, RateDistortionLoss against that same batch (:349-351), backward,
     clip_grad_norm_(1.0) over the main parameters (:360), Adam(lr_train) (:361), then the aux loss of the
     EntropyBottleneck quantiles and its Adam(1e-3) (:363-366; coder.py:50-86 optimiser split).
-    Returns (updated params dict, loss values, aux loss, the adversarial batch); record: the inner attack's per-step
-    records (attack())."""
+    Returns (updated params dict, loss values (with the pre-clip gradient norm "grad_norm"), aux loss, the
+    adversarial batch); record: the inner attack's per-step records (attack()).  state: a dict that carries the
+    parameters and both Adam optimisers from one call to the next (several outer steps of one run; P is read on the
+    first call only)."""
     r = attack(P, batch_x, steps=steps, epsilon=epsilon, noise_thr=noise_thr, lr=lr_attack, att_metric=att_metric,
                clamp=clamp, model=model, coupled=True, eval_msssim=False, record=record)
     batch_adv = r.im_adv.detach()
     main_names = sorted(k for k in P if not k.endswith(".quantiles"))
     aux_names = sorted(k for k in P if k.endswith(".quantiles"))
-    Q = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
-    opt = torch.optim.Adam([Q[k] for k in main_names], lr=lr_train)
-    aux_opt = torch.optim.Adam([Q[k] for k in aux_names], lr=1e-3)
+    if state is not None and "Q" in state:
+        Q, opt, aux_opt = state["Q"], state["opt"], state["aux_opt"]
+    else:
+        Q = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
+        opt = torch.optim.Adam([Q[k] for k in main_names], lr=lr_train)
+        aux_opt = torch.optim.Adam([Q[k] for k in aux_names], lr=1e-3)
+        if state is not None:
+            state.update(Q=Q, opt=opt, aux_opt=aux_opt)
     res = codec.forward(Q, batch_adv, model, training=True, noise_y=noise_y, noise_z=noise_z)
     out = rd_loss(res, batch_adv, metric, lmbda)
     opt.zero_grad()
     aux_opt.zero_grad()
     out["loss"].backward()
-    torch.nn.utils.clip_grad_norm_([Q[k] for k in main_names], 1.0)
+    gn = torch.nn.utils.clip_grad_norm_([Q[k] for k in main_names], 1.0)
     opt.step()
+    out["grad_norm"] = gn
     aux_loss = codec.eb_aux_loss(Q)
     aux_opt.zero_grad()
     aux_loss.backward()
     aux_opt.step()
-    return ({k: v.detach() for k, v in Q.items()}, {k: float(v) for k, v in out.items()}, float(aux_loss),
+    return ({k: v.detach() for k, v in Q.items()}, {k: float(v.detach()) for k, v in out.items()}, float(aux_loss),
             batch_adv)

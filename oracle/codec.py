@@ -358,8 +358,22 @@ def context_mask(k=5):
 
 
 def context_prediction(P, y_hat):
-    w = P["context_prediction.weight"] * context_mask(P["context_prediction.weight"].shape[-1])
+    """CompressAI's MaskedConv2d.forward: ``self.weight.data *= self.mask`` (in place, outside autograd), then the
+    plain conv on the parameter, so the weight's gradient is the UNMASKED conv weight gradient (all 25 taps) and the
+    masked taps' gradients enter clip_grad_norm_ (reference train.py:360)."""
+    w = P["context_prediction.weight"]
+    with torch.no_grad():
+        w.mul_(context_mask(w.shape[-1]).to(w.dtype))
     return F.conv2d(y_hat, w, P["context_prediction.bias"], padding=w.shape[-1] // 2)
+
+
+def joint_noise(noise_y):
+    """Train-mode noise of the joint-prior models: (for y_hat = quantize(y, "noise"), for the GaussianConditional's
+    own requantisation).  CompressAI draws the two independently (JointAutoregressiveHierarchicalPriors.forward);
+    None draws both, a pair pins both, and one tensor pins a shared draw (the pinned mode of the round-5 tests)."""
+    if isinstance(noise_y, (tuple, list)):
+        return noise_y[0], noise_y[1]
+    return noise_y, noise_y
 
 
 def entropy_parameters(P, t):
@@ -374,14 +388,15 @@ def cheng_forward(P, x, training=False, noise_y=None, noise_z=None):
     z = cheng_h_a(P, y)
     z_hat, z_lik = entropy_bottleneck(P, z, training, noise_z)
     params = cheng_h_s(P, z_hat)
+    ny_hat, ny_lik = joint_noise(noise_y)
     if training:
-        y_hat = y + (noise_y if noise_y is not None else torch.empty_like(y).uniform_(-0.5, 0.5))
+        y_hat = y + (ny_hat if ny_hat is not None else torch.empty_like(y).uniform_(-0.5, 0.5))
     else:
         y_hat = torch.round(y)   # quantize(y, "dequantize") with means=None
     ctx = context_prediction(P, y_hat)
     gp = entropy_parameters(P, torch.cat((params, ctx), dim=1))
     scales, means = gp.chunk(2, 1)
-    _, y_lik = gaussian_conditional(y, scales, means, training, noise_y)
+    _, y_lik = gaussian_conditional(y, scales, means, training, ny_lik)
     return {"x_hat": cheng_g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
 
 
@@ -408,14 +423,15 @@ def mbt_forward(P, x, training=False, noise_y=None, noise_z=None):
     z = mbt_h_a(P, y)
     z_hat, z_lik = entropy_bottleneck(P, z, training, noise_z)
     params = mbt_h_s(P, z_hat)
+    ny_hat, ny_lik = joint_noise(noise_y)
     if training:
-        y_hat = y + (noise_y if noise_y is not None else torch.empty_like(y).uniform_(-0.5, 0.5))
+        y_hat = y + (ny_hat if ny_hat is not None else torch.empty_like(y).uniform_(-0.5, 0.5))
     else:
         y_hat = torch.round(y)
     ctx = context_prediction(P, y_hat)
     gp = entropy_parameters(P, torch.cat((params, ctx), dim=1))
     scales, means = gp.chunk(2, 1)
-    _, y_lik = gaussian_conditional(y, scales, means, training, noise_y)
+    _, y_lik = gaussian_conditional(y, scales, means, training, ny_lik)
     return {"x_hat": g_s(P, y_hat), "likelihoods": {"y": y_lik, "z": z_lik}}
 
 

@@ -57,7 +57,8 @@ def test_rd_backward_vs_oracle(model, metric, H, W, q, lmbda):
     torch.cuda.synchronize()
     ref, grads = _oracle_grads(P, x, model, metric, lmbda, ny, nz)
     for k in ("loss", "bpp_loss", "distortion_loss"):
-        assert abs(float(got[k]) - float(ref[k])) <= 1e-4 * max(abs(float(ref[k])), 1.0), k
+        r = float(ref[k].detach())
+        assert abs(float(got[k]) - r) <= 1e-4 * max(abs(r), 1.0), k
     named = dict(net.named_parameters())
     checked = 0
     worst = []

@@ -109,7 +109,8 @@ def test_joint_rd_backward_vs_float64(model, q, metric, H, W, monkeypatch):
     torch.cuda.synchronize()
     ref, grads, dis = _f64_with_path_kinks(P, x, ny, nz, metric, lmbda, masks, monkeypatch, model)
     for k in ("loss", "bpp_loss", "distortion_loss"):
-        assert abs(float(got[k]) - float(ref[k])) <= 1e-5 * max(abs(float(ref[k])), 1.0), k
+        r = float(ref[k].detach())
+        assert abs(float(got[k]) - r) <= 1e-5 * max(abs(r), 1.0), k
     worst, checked = [], 0
     for k, g64 in grads.items():
         if k.endswith(".quantiles"):
@@ -191,3 +192,81 @@ def test_joint_adv_train_step_vs_oracle(model):
     print("worst parameter moves (max, p99.9 in steps):", worst[:3])
     assert worst[0][0] <= 2.0, worst[:3]
     assert max(w[1] for w in worst) <= 1e-2, sorted(worst, key=lambda w: -w[1])[:3]
+
+
+@pytest.mark.parametrize("model", ["cheng2020", "context"])
+def test_joint_adv_train_two_steps_clipped(model):
+    """Two outer steps of train.py --adv (one Adam state across them) vs oracle.attack.adv_train_step, with lambda
+    large enough that clip_grad_norm_(1.0) is active (reference train.py:360): the pre-clip norm of every main gradient
+    matches the oracle's to 2e-5 (measured 2-4e-6).  The masked context taps keep their gradient, as CompressAI's
+    MaskedConv2d (it masks weight.data, outside autograd): their clipped gradient must equal the oracle's (1e-3 of its
+    max) and be non-zero.  (Their share of the clipped norm is ~1e-6 here, printed: the norm alone could not tell.)
+    Independent y_hat / likelihood noise per step (CompressAI's two draws).  After the second Adam step the parameter moves are compared in direction (cosine) and
+    median: per element, Adam's m / sqrt(v) over two clipped gradients amplifies the fp32 oracle's own leaky-ReLU-kink
+    gradient noise (up to ~4e-3 of max: test_joint_rd_backward_vs_float64) where the two steps' gradients cancel."""
+    from types import SimpleNamespace
+    from imagecompression_adversarial_amd import coder
+    from imagecompression_adversarial_amd.train import adv_step
+    from imagecompression_adversarial_amd.train_engine import RDTrainer
+    q, steps, B, H, W = 6, 2, 2, 64, 64
+    P = oc.perturb_params(oc.init_params(model, q, seed=0), seed=1)
+    N, M = oc.model_channels(model, q)
+    lr_train, metric, lmbda = 1e-4, "mse", 2.0
+    net = _net(P, q, model)
+    opt, aux = coder.configure_optimizers(net, SimpleNamespace(adv=True, lr_train=lr_train))
+    tr = RDTrainer(net, metric, lmbda)
+    # a 1e-3/255 L-inf box: the inner attack runs, but its leaky-ReLU-kink sign flips (tests/test_gpu_cheng.py) cannot
+    # move the batch by more than 8e-6, so the two outer steps compare the RD step, clip and Adam, not the attack
+    eps = 1e-3
+    args = SimpleNamespace(steps=steps, epsilon=eps, noise=1e-4, lr_attack=0.01, att_metric="L2", clamp=True,
+                           round_adv=False)
+    state = {}
+    P0 = {k: v.clone() for k, v in P.items()}   # the oracle's eval forwards zero P's masked taps in place
+    named0 = dict(net.named_parameters())
+    p0 = {k: v.detach().cpu().clone() for k, v in named0.items()}
+    for o in range(2):
+        x = rnd((B, 3, H, W), 60 + o)
+        ny = (rnd((B, M, H // 16, W // 16), 70 + o, -0.5, 0.5), rnd((B, M, H // 16, W // 16), 80 + o, -0.5, 0.5))
+        nz = rnd((B, N, H // 64, W // 64), 90 + o, -0.5, 0.5)
+        out, adv = adv_step(net, tr, opt, aux, x.to(DEV), args, qnoise=(tuple(t.to(DEV) for t in ny), nz.to(DEV)))
+        torch.cuda.synchronize()
+        Pn, ref_out, _, ref_adv = oa.adv_train_step(P, x, steps=steps, epsilon=eps, model=model, metric=metric,
+                                                     lmbda=lmbda, lr_train=lr_train, noise_y=ny, noise_z=nz,
+                                                     state=state)
+        gn, gr = float(out["grad_norm"]), float(ref_out["grad_norm"])
+        ea = rel_err(adv.cpu(), ref_adv)
+        print(f"outer step {o}: grad norm HIP {gn:.4f} oracle {gr:.4f}; adversarial batch {ea:.1e}; loss "
+              f"{float(out['loss']):.6f} vs {ref_out['loss']:.6f}")
+        assert gr > 1.0, "clip_grad_norm_ inactive: raise lambda"
+        assert ea < 1e-4, ea
+        mask = 1 - oc.context_mask(5)
+        gc = named0["context_prediction.weight"].grad.detach().cpu() * mask   # clipped: the total norm is now 1
+        gco = state["Q"]["context_prediction.weight"].grad.detach() * mask
+        print(f"  masked-tap share of the clipped gradient {float(gc.norm()):.3e}, vs oracle {rel_err(gc, gco):.1e}")
+        assert float(gco.abs().max()) > 0 and rel_err(gc, gco) < 1e-3
+        assert abs(gn - gr) <= 2e-5 * gr, (gn, gr)
+        for k in ("loss", "bpp_loss", "distortion_loss"):
+            assert abs(float(out[k]) - ref_out[k]) <= 1e-4 * max(abs(ref_out[k]), 1.0), k
+    named = named0
+    mh, mo, dd = [], [], []
+    for k, v in Pn.items():
+        if k.endswith(".quantiles"):
+            continue
+        a = (named[k].detach().cpu().reshape(v.shape) - p0[k].reshape(v.shape)).flatten()
+        b = (v - P0[k].reshape(v.shape)).flatten()
+        mh.append(a)
+        mo.append(b)
+        dd.append((a - b).abs() / lr_train)
+    names = [k for k in Pn if not k.endswith(".quantiles")]
+    per = sorted(((float(d.max()), float(m.abs().max()) / lr_train, float(o.abs().max()) / lr_train, k)
+                  for d, m, o, k in zip(dd, mh, mo, names)), reverse=True)
+    print("largest move differences (max |d|, max |HIP move|, max |oracle move|, in steps):", per[:4])
+    mh, mo, dd = torch.cat(mh).double(), torch.cat(mo).double(), torch.cat(dd).double()
+    cos = float(mh @ mo / (mh.norm() * mo.norm()))
+    med = float(dd.median())
+    print(f"parameter moves after two steps: cosine {cos:.6f}, median |d| {med:.2e} steps, p99 "
+          f"{float(torch.quantile(dd[:1 << 24], 0.99)):.2e}")
+    assert cos > 0.999, cos
+    assert med <= 1e-2, med
+    w = named["context_prediction.weight"].detach().cpu()
+    assert float((w * (1 - oc.context_mask(5))).abs().max()) > 0, "the masked taps must move (unmasked gradient)"
