@@ -26,6 +26,7 @@ random start (the reference default path), per image.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -36,6 +37,14 @@ from . import hip_ops as K
 from . import msssim as MS
 from ._lib import call, ptr, stream
 from .engine import CodecKernels
+
+
+# HIP-graph replay of the whole-batch network step (g_a, g_s, loss, g_s^T, g_a^T: ~25 launches) while every image
+# stays on the expensive branch: captured once per AttackLoop (its weights and buffers are fixed), replayed by one
+# launch per step.  The replay runs the captured kernels on the same buffers, so the bits equal the eager step's
+# (tests/test_gpu_graph.py).  ICA_ATTACK_GRAPH=0 turns it off.
+ATTACK_GRAPH = os.environ.get("ICA_ATTACK_GRAPH", "1") != "0"
+GRAPH_STATS = {"captures": 0, "replays": 0}   # process-wide counters (bench.py --config 4 reports them)
 
 
 def _lr_table(steps, lr):
@@ -184,6 +193,10 @@ class AttackLoop:
         # wall time spent blocked in those waits (bench.py --mixed reports them)
         self.sync_steps = 0
         self.sync_wait_s = 0.0
+        # the whole-batch network step as a HIP graph (L2 losses; the ms-ssim loss path and the ROI attack run eager)
+        self.graph_ok = ATTACK_GRAPH and dev.type == "cuda" and att_metric == "L2" and target is None
+        self._graph, self._graph_out = None, None
+        self.graph_replays = 0
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
         if pad:
             # -p P (attack_rd.py:389-413): the pre-eval codes the image padded by P (-padmode, reflect by default),
@@ -277,6 +290,26 @@ class AttackLoop:
         del ss, xh4
         return kern.g_a_backward(gy4, sa)
 
+    def _network_graph(self):
+        """network_grad() on the whole batch through a HIP graph: captured on first use (the capture does not run
+        the kernels, so it is replayed right away), one replay per step after that.  The per-launch timing hooks of
+        hip_ops (bench.py) see only the eager launches."""
+        if self._graph is None:
+            hooks = (K.EVENT_HOOK, K.LAUNCH_HOOK)
+            K.EVENT_HOOK = K.LAUNCH_HOOK = None
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, capture_error_mode="relaxed"):
+                    out = self.network_grad(None, self.B)
+            finally:
+                K.EVENT_HOOK, K.LAUNCH_HOOK = hooks
+            self._graph, self._graph_out = g, out
+            GRAPH_STATS["captures"] += 1
+        self._graph.replay()
+        self.graph_replays += 1
+        GRAPH_STATS["replays"] += 1
+        return self._graph_out
+
     def step(self, i, record_im_in=False, census=False):
         B, H, W = self.B, self.H, self.W
         if self.roi is not None:
@@ -287,7 +320,10 @@ class AttackLoop:
         if self.coupled:
             D.couple_loss_i(self.loss_i, self.B_global, self.group)
         E, idx = self._select()
-        gx4 = self.network_grad(idx, E) if E > 0 else None
+        if E == B and idx is None and self.graph_ok:
+            gx4 = self._network_graph()
+        else:
+            gx4 = self.network_grad(idx, E) if E > 0 else None
         cheap_grad = None
         if self.metric == "ms-ssim" and E < B:
             # cheap branch loss = 1 - ms_ssim(im_s, im_in): d/d im_in = -dMS/dY

@@ -5,6 +5,12 @@
 #pragma once
 #include "ica_common.h"
 
+// A/B builds only (scripts/build_variant.sh): 1 = the conv_epilogue x6 GDN / IGDN forward with the fp32 path's IEEE
+// 1/sqrtf / sqrtf instead of v_rsq_f32 / v_sqrt_f32 (the cheng2020 k3 kernels)
+#ifndef ICA_X6_IEEE_GDN
+#define ICA_X6_IEEE_GDN 0
+#endif
+
 enum {
   EPI_BIAS = 0,      // y = acc + bias
   EPI_RELU = 1,      // y = relu(acc + bias)
@@ -415,7 +421,7 @@ ICA_DEV void conv_epilogue(const ConvParams& p, f32x16 (&acc)[IT], int n, int oy
             float s;
             // x6: the same 1-ulp instructions (1/sqrtf rounds twice, so the IEEE form is no closer; measured
             // 8-10k cycles per conv_up class of IEEE sqrt fix-ups)
-            if constexpr (BF || X6) s = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
+            if constexpr (BF || (X6 && !ICA_X6_IEEE_GDN)) s = (EPI == EPI_GDN) ? __builtin_amdgcn_rsqf(nv) : __builtin_amdgcn_sqrtf(nv);
             else s = (EPI == EPI_GDN) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
             sv[e] = s;
             yv[e] = acc[ct][4 * g + e] * s;

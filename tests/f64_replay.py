@@ -44,6 +44,12 @@ def replay64(P, x, steps, monkeypatch, with_log=False, **kw):
 
 
 ILL = 1e-4   # an element is ill-conditioned when its float64 gradient falls below ILL of the step's max
+ILL_BOUND = 3e-3   # the largest deviation (of max|noise64|) an ill-conditioned element may take
+
+
+def ill_set_size(gmin):
+    """Number of noise elements in the ill-conditioned set (float64 |g| < ILL of the step max at some step)."""
+    return int((gmin < ILL).sum())
 
 
 def confined(noise, res64, gmin, tol=1e-3):

@@ -556,11 +556,12 @@ def test_cheng_attack_seeds_vs_float64(cheng6, cheng6x6, seed, path, monkeypatch
     wrong away from zero), every branch kept, the output at the fp32 tolerance, and every noise element within 1e-3 of
     the float64 noise max -- except elements the float64 trajectory itself does not determine at fp32 resolution: those
     whose float64 gradient falls below ILL = 1e-4 of the step's max|g| at some step, where Adam's g / (|g| + 1e-8)
-    turns an fp32-level gradient error into an O(lr) step (measured: x6 seed 38, one such element at 1.7e-3),
-    bounded at 1e-2.  (Round 4 matched kinks at step 0 only; seed 38 then crossed a step-3 kink the
+    turns an fp32-level gradient error into an O(lr) step, bounded at ILL_BOUND = 3e-3 (round 5 measured x6 seed 38
+    at 1.7e-3 and, in the 24-seed sweep, seeds 116 / 121 at 1.9e-3 / 1.1e-3, one element each).  The test message
+    and the sweep print the size of the ill-conditioned set (of 24576 noise elements) per seed and path.  (Round 4 matched kinks at step 0 only; seed 38 then crossed a step-3 kink the
     replay did not take -- fp32 23 elements beyond, max 2.3e-2 -- and its gate fell back to comparing x6 with the fp32
     HIP path.)"""
-    from tests.f64_replay import KINK_REL, confined, replay64_path_kinks
+    from tests.f64_replay import ILL_BOUND, KINK_REL, confined, ill_set_size, replay64_path_kinks
     P, kern = cheng6 if path == "fp32" else cheng6x6
     x = rnd((2, 3, 64, 64), seed, 0.0, 1.0)
     noise, output_s, branches, r64, gmin, rec, per_step = replay64_path_kinks(
@@ -569,11 +570,13 @@ def test_cheng_attack_seeds_vs_float64(cheng6, cheng6x6, seed, path, monkeypatch
         assert [bool(v) for v in br] == [bool(v) for v in rec[i]["cheap"]], i
     n_bad, n_bad_well, dmax = confined(noise, r64, gmin)
     steps = {i: ([len(f) for f in fl], [f"{w:.1e}" for w in wo]) for i, (fl, wo) in per_step.items()}
+    n_ill = ill_set_size(gmin)
     print(f"{path} seed {seed}: kinks taken per network step (per image count, largest disagreement) {steps}; "
-          f"{n_bad} elements beyond 1e-3 of the float64 noise ({n_bad_well} well-conditioned), max {dmax:.3e}")
+          f"{n_bad} elements beyond 1e-3 of the float64 noise ({n_bad_well} well-conditioned), max {dmax:.3e}; "
+          f"ill-conditioned set {n_ill} of {gmin.numel()}")
     d = (noise.double().cpu() - r64.noise).abs() / r64.noise.abs().max()
     for e in (d > 1e-3).flatten().nonzero().flatten().tolist():
         print(f"  element {e}: deviation {float(d.flatten()[e]):.2e}, float64 min |g| / max|g| {float(gmin.flatten()[e]):.1e}")
     assert all(w < KINK_REL for _, wo in per_step.values() for w in wo), per_step
     assert rel_err(output_s.cpu(), r64.output_s.float()) < 2e-4
-    assert n_bad_well == 0 and dmax <= 1e-2, (n_bad, n_bad_well, dmax)
+    assert n_bad_well == 0 and dmax <= ILL_BOUND, (n_bad, n_bad_well, dmax, n_ill)
