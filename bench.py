@@ -456,9 +456,14 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    from imagecompression_adversarial_amd import attack as A
     from imagecompression_adversarial_amd import codec as models
     from imagecompression_adversarial_amd import hip_ops as K
     from imagecompression_adversarial_amd.attack import AttackLoop
+    # the timed steps run eager, so that every tagged launch is bracketed by its own HIP events (the roofline's
+    # per-launch time over the timed region); the product's graph replay of the network step (attack.py) is off
+    # here unless ICA_BENCH_GRAPH=1 (then per_kernel_ms / roofline come from eager launches only and are absent)
+    A.ATTACK_GRAPH = os.environ.get("ICA_BENCH_GRAPH", "0") == "1"
     from imagecompression_adversarial_amd.engine import CodecKernels
     from imagecompression_adversarial_amd.engine_cheng import ChengKernels
 
