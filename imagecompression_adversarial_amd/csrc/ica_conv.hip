@@ -809,8 +809,14 @@ __global__ __launch_bounds__(256, 2) void conv_down_split_kernel(ConvParams p) {
 // bf16 path doubles the rows: each wave then runs two 32-pixel tiles per class (up_pt), so a weight
 // fragment feeds twice the MFMAs (as in conv_down).
 constexpr int UP_TW = 16, UP_PC = UP_TW + 2;
+#ifndef ICA_BF_UP3_OLD
+#define ICA_BF_UP3_OLD 0   // A/B builds: 1 = the bf16 Z-gather on conv_up3_kernel<true> (rounds 1-5)
+#endif
+#ifndef ICA_BF_UP_PT
+#define ICA_BF_UP_PT 2   // A/B builds: pixel tiles per wave and class of the bf16 conv_up (4: one block per CU)
+#endif
 template <bool BF>
-constexpr int up_pt() { return BF ? 2 : 1; }
+constexpr int up_pt() { return BF ? ICA_BF_UP_PT : 1; }
 template <bool BF>
 constexpr int up_th() { return 4 * up_pt<BF>(); }
 template <bool BF>
@@ -1006,7 +1012,7 @@ ICA_DEV void conv_up_pair(const ConvParams& p, const f32x4* patch, int n, int a0
 }
 
 template <int KS, int IT, int EPI, int FX, bool BF>
-__global__ __launch_bounds__(256, (conv_min_blocks<KS, IT>())) void conv_up_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, ((BF && ICA_BF_UP_PT > 2) ? 1 : conv_min_blocks<KS, IT>())) void conv_up_kernel(ConvParams p) {
   ICA_STAMP_BEGIN();
   extern __shared__ f32x4 patch[];  // fp32: [Cin/4][TH+2][UP_PC] f32x4; bf16: [Cin/8][TH+2][UP_PC] bf16x8
   constexpr int UP_TH = up_th<BF>(), UP_PLANE = up_plane<BF>();
@@ -1430,7 +1436,11 @@ constexpr int u3_rows() { return 4 * CT - 2; }
 template <int CT>
 constexpr int u3_npx() { return 4 * CT * U3_HW; }
 
-template <int NCH, int CT>
+// BF: the same persistent pipeline on bf16 operands (config 5's g_s.6 forward / g_a.0 input gradient; bf16 nChw4c
+// activations, 8-B channel quads; the ica_pack_up3_bf16 fragments, one plane): one MFMA per chunk and row tile, no
+// split.  It replaced conv_up3_kernel<true> (one block of 5 x 32 input pixels, loads up front, 1.2 ms per launch at
+// the config-5 shapes).
+template <int NCH, int CT, bool BF = false>
 __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p) {
   constexpr int R = u3_rows<CT>(), NPX = u3_npx<CT>();
   __shared__ float zs[T3_ROWS * NPX];
@@ -1462,27 +1472,35 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p) {
   // quad 2h), or OOB for pixels outside the image and for the "next tile" past the block's run (the loads then
   // return zeros: no branches in the MFMA loop)
   const bool split_in = (p.pl & PL_IN) != 0;
-  const unsigned qs = plane * 16u, cs = 4u * qs;   // second quad, next chunk (bytes)
+  constexpr unsigned QB = BF ? 8u : 16u;             // bytes per channel quad
+  const unsigned qs = plane * QB, cs = 4u * qs;      // second quad, next chunk (bytes)
   constexpr unsigned OOB = 0xFFFFFFF0u;
   auto prep = [&](int t, bool real, __amdgpu_buffer_rsrc_t& r, unsigned (&vb)[CT]) __attribute__((always_inline)) {
     int n, a0, b0;
     coords(real ? t : t_begin, n, a0, b0);
-    r = uniform_rsrc(p.x + (size_t)n * Cin4 * plane * 4, (unsigned)(Cin4 * plane * 16));
+    r = uniform_rsrc(reinterpret_cast<const char*>(p.x) + (size_t)n * Cin4 * plane * QB, (unsigned)(Cin4 * plane * QB));
     const int ix = b0 - 1 + j;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int iy = a0 - 1 + wave + 4 * ct;
       const bool ok = real && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      vb[ct] = ok ? ((unsigned)(2 * h) * plane + pix_at(iy, ix, p.Hin, p.Win, split_in)) * 16u : OOB;
+      vb[ct] = ok ? ((unsigned)(2 * h) * plane + pix_at(iy, ix, p.Hin, p.Win, split_in)) * QB : OOB;
     }
   };
-  f32x4 xa[CT][NCH][2];
+  // fp32: two 16-B quads (8 channels) per (ct, ch); bf16: two 8-B quads, packed into the first
+  f32x4 xa[CT][NCH][BF ? 1 : 2];
   auto load = [&](const __amdgpu_buffer_rsrc_t& r, const unsigned (&vb)[CT], int ct, int ch)
       __attribute__((always_inline)) {
     const bool ok = vb[ct] != OOB;
     const unsigned o = vb[ct] + (unsigned)ch * cs;
-    xa[ct][ch][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? o : OOB, 0, 0));
-    xa[ct][ch][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? o + qs : OOB, 0, 0));
+    if constexpr (BF) {
+      const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, ok ? o : OOB, 0, 0));
+      const u32x2 hi = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, ok ? o + qs : OOB, 0, 0));
+      xa[ct][ch][0] = __builtin_bit_cast(f32x4, (u32x4_t){lo[0], lo[1], hi[0], hi[1]});
+    } else {
+      xa[ct][ch][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? o : OOB, 0, 0));
+      xa[ct][ch][BF ? 0 : 1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? o + qs : OOB, 0, 0));
+    }
   };
   __amdgpu_buffer_rsrc_t rn;
   unsigned vbn[CT];
@@ -1492,18 +1510,24 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) load(rn, vbn, ct, ch);
   constexpr long pst = 3L * NCH * 64;   // fragments per plane
-  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(3 * pst * 16));
+  constexpr int NPL = BF ? 1 : 3;        // weight planes
+  const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)(NPL * pst * 16));
   int wz = 0;   // a per-tile "zero" (keeps the fragment offsets from being hoisted into SGPRs across the tile loop)
   auto ldw = [&](bf16x8 (&a)[3][3], int ch) {
 #pragma unroll
     for (int it = 0; it < 3; ++it)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, wz + (int)((q * pst + ((long)it * NCH + ch) * 64) * 16));
+      for (int q = 0; q < NPL; ++q) a[it][q] = ld_bf8(wr, lane * 16, wz + (int)((q * pst + ((long)it * NCH + ch) * 64) * 16));
   };
   auto split = [&](int ct, int ch, bf16x8 (&b)[3]) __attribute__((always_inline)) {
-    const float v[8] = {xa[ct][ch][0][0], xa[ct][ch][0][1], xa[ct][ch][0][2], xa[ct][ch][0][3],
-                        xa[ct][ch][1][0], xa[ct][ch][1][1], xa[ct][ch][1][2], xa[ct][ch][1][3]};
-    split3x8(v, b);
+    if constexpr (BF) {
+      b[0] = f4_as_bf8(xa[ct][ch][0]);
+    } else {
+      const float v[8] = {xa[ct][ch][0][0], xa[ct][ch][0][1], xa[ct][ch][0][2], xa[ct][ch][0][3],
+                          xa[ct][ch][BF ? 0 : 1][0], xa[ct][ch][BF ? 0 : 1][1], xa[ct][ch][BF ? 0 : 1][2],
+                          xa[ct][ch][BF ? 0 : 1][3]};
+      split3x8(v, b);
+    }
   };
   const float bias0 = p.bias ? p.bias[0] : 0.f, bias1 = p.bias ? p.bias[1] : 0.f, bias2 = p.bias ? p.bias[2] : 0.f;
 #pragma unroll 1
@@ -1532,14 +1556,19 @@ __global__ __launch_bounds__(256, 1) void conv_up3_x6p_kernel(ConvParams p) {
         bf16x8 bn[3];
         if (nch < NCH) split(nct, nch, bn);
 #pragma unroll
-        for (int it = 0; it < 3; ++it) acc[ct][it] = mfma_x6(wa[ch & 1][it], bc, acc[ct][it]);
-        load(rn, vbn, ct, ch);   // the registers just consumed take tile t+1's chunk
-#pragma unroll
-        for (int k = 0; k < 18; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // up to three VALU (the next operand's split)
+        for (int it = 0; it < 3; ++it) {
+          if constexpr (BF) acc[ct][it] = mfma32bf(wa[ch & 1][it][0], bc[0], acc[ct][it]);
+          else acc[ct][it] = mfma_x6(wa[ch & 1][it], bc, acc[ct][it]);
         }
-        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // the two activation loads
+        load(rn, vbn, ct, ch);   // the registers just consumed take tile t+1's chunk
+        if constexpr (!BF) {
+#pragma unroll
+          for (int k = 0; k < 18; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // up to three VALU (the next operand's split)
+          }
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // the two activation loads
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (nch < NCH) {
 #pragma unroll
@@ -2282,6 +2311,13 @@ int ica_conv_up3_bf16(const float* x, float* y, const void* wp, const float* bia
   ConvParams p{x, y, reinterpret_cast<const float*>(wp), bias, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                N, Cin, Hin, Win, 3, 2 * Hin, 2 * Win, nullptr};
   p.pl = layout;
+  if (Cin == 128 && !ICA_BF_UP3_OLD) {   // the persistent pipeline (conv_up3_x6p_kernel<.., BF>)
+    const int tiles = ((Win + U3_OW - 1) / U3_OW) * ((Hin + u3_rows<3>() - 1) / u3_rows<3>()) * N;
+    const int nb = std::max(1, std::min((tiles + 7) / 8, ica_cu_count() / 8));
+    ICA_LAUNCH((conv_up3_x6p_kernel<8, 3, true>), dim3(8 * nb), dim3(256), 0, st, p);
+    ICA_CHECK_LAUNCH();
+    return 0;
+  }
   const int tiles = ((Win + T3_TW - 1) / T3_TW) * ((Hin + T3_TH - 1) / T3_TH) * N;
   ICA_LAUNCH(conv_up3_kernel<true>, dim3(tiles), dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();

@@ -73,7 +73,10 @@ int ica_pack_gdn_bf16(const float* gamma, const float* beta, void* gpb, float* b
  * ica_pack_conv_weight (order 0: conv_down, 1: conv_up) with row tiles it (> 0).  For KS = 5, it = 4 the buffer
  * continues with the tap-pair pack of the 8-wave conv_down (three planes of [cb][K step][it][lane] fragments; lane half
  * h of a step = tap 2 s + h of an 8-channel chunk, chunk pairs sharing a tap-24 step; filled for order 0);
- * ica_pack_conv_weight_x6_size(O, C, KS, it) bf16 values in all. */
+ * ica_pack_conv_weight_x6_size(O, C, KS, it) bf16 values in all.  Order 2 (KS = 5, C <= 3: the RGB-side conv_down
+ * of g_a.0 forward / the g_s.6 input gradient, 128 output channels) packs the dense tap-row K of conv_rgb5_x6
+ * instead: three planes of [cb][ky][it][lane] fragments, k = 8 h + e of step ky holding (kx, c) = h 0: (0..1, 0..2),
+ * (4, 0..1); h 1: (2..3, 0..2), (4, 2), zero; it fits in the size above.  Returns -2 for order 2 with other shapes. */
 int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, long so, long sc, int order, int it,
                             hipStream_t stream);
 size_t ica_pack_conv_weight_x6_size(int O, int C, int KS, int it);
