@@ -2099,6 +2099,8 @@ static int pick_up(const ConvParams& p, int KS, int it, int epi, int fx, hipStre
 
 // fp32-accurate bf16x6 operand kernels (ica_conv_x6.hip)
 int ica_conv_x6_dispatch(const ConvParams& p, int kind, int KS, int S, int it, int epi, int fx, hipStream_t st);
+int ica_rgb5_bf16_dispatch(const ConvParams& p, int epi, hipStream_t st);
+int ica_pack_rgb5_planes(const float* w, void* dst, int O, int C, long so, long sc, int it, int planes, hipStream_t st);
 
 // C-ABI argument block of ica_conv_ex (mirrors include/ica_hip.h)
 extern "C" {
@@ -2213,6 +2215,10 @@ int ica_pack_conv_weight_bf16(const float* w, void* dst, int O, int C, int KS, l
                               int it, hipStream_t st) {
   const int IT = resolve_it(O, it);
   if (C <= 4) {  // conv_down tap groups (RGB input)
+    if (order == 2) {   // the dense tap-row pack of conv_rgb5_bf16 (C <= 3, KS = 5, no flip): one bf16 plane
+      if (KS != 5 || flip) return -4;
+      return ica_pack_rgb5_planes(w, dst, O, C, so, sc, IT, 1, st);
+    }
     if (order != 0) return -4;
     const long tot = (long)ica_pack_conv_weight_bf16_size(O, C, KS, IT);
     ICA_LAUNCH(pack_conv_tg_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
@@ -2427,6 +2433,10 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
     }
     return ica_conv_x6_dispatch(p, a->kind, a->KS, a->S, it, a->epi, fx, st);
   }
+  // bf16 RGB-side conv_down with the dense tap-row pack (hip_ops packs order 2 for exactly these layers)
+  if (a->prec == 1 && a->kind == 0 && a->KS == 5 && a->S == 2 && a->Cin <= 3 && a->Cout == 128 && it == 4 && fx == 0 &&
+      a->fill_mode == 0 && (a->epi == EPI_BIAS || a->epi == EPI_GDN || a->epi == EPI_IGDN_BWD))
+    return ica_rgb5_bf16_dispatch(p, a->epi, st);
   if (a->kind == 0) return pick_down(p, a->KS, a->S, it, a->epi, fx, st);
   if (a->kind == 1) return a->S == 2 ? pick_up(p, a->KS, it, a->epi, fx, st) : -6;
   return -6;

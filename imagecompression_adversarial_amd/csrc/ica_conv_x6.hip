@@ -1002,6 +1002,69 @@ __global__ __launch_bounds__(256, 1) void conv_rgb5w_x6_kernel(ConvParams p, lon
   }
 }
 
+// bf16 operands (config 5's RGB end, the targeted ROI attack's g_a.0 forward / g_s.6 input gradient): the same dense
+// tap-row K and persistent row-tile walk; B = the 8 RGB values rounded to bf16 (one plane), weights one bf16 plane
+// (plane 0 of the x6 split = round-to-nearest bf16(w)), the bf16 conv path's epilogues (bf16 y / s / dx nChw4c;
+// bias, beta' and the gamma' / gamma'^T hi fragments from LDS: epi_params_to_lds).  7 tap-group MFMAs per tile
+// (pack_conv_tg_kernel) become 5; the per-tile weight fragment loads become one LDS copy per CU.
+constexpr int RGB5B_W_BYTES = RGB5_KY * RGB5_IT * 64 * 16;   // 20480
+
+template <int EPI>
+constexpr int rgb5b_lds_bytes() { return RGB5B_W_BYTES + epi_lds_entries<RGB5_IT, EPI>() * 16; }
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void conv_rgb5_bf16_kernel(ConvParams p, int nblk) {
+  extern __shared__ __attribute__((aligned(16))) char rgb5_lds[];
+  constexpr int IT = RGB5_IT;
+  {
+    const __amdgpu_buffer_rsrc_t wr = uniform_rsrc(p.wp, (unsigned)RGB5B_W_BYTES);
+    for (int e = threadIdx.x; e < RGB5B_W_BYTES / 16; e += blockDim.x)
+      *reinterpret_cast<f32x4*>(rgb5_lds + (size_t)e * 16) =
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, e * 16, 0, 0));
+  }
+  const f32x4* lp = reinterpret_cast<const f32x4*>(rgb5_lds + RGB5B_W_BYTES);
+  if (threadIdx.x < 256) epi_params_to_lds<IT, EPI>(p, reinterpret_cast<f32x4*>(rgb5_lds + RGB5B_W_BYTES), 0);
+  __syncthreads();
+  const int tiles_x = (p.Wout + 31) / 32, total = tiles_x * p.Hout * p.N, per = (total + nblk - 1) / nblk;
+  int b, cb;
+  xcd_block<true>(b, cb);
+  const int t_end = min(total, b * per + per), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+#pragma unroll 1
+  for (int t = b * per + wave; t < t_end; t += 8) {
+    const int tx = t % tiles_x, r = t / tiles_x;
+    const int oy = r % p.Hout, n = r / p.Hout, ox = tx * 32 + (threadIdx.x & 31);
+    const bool valid = ox < p.Wout;
+    f32x4 q[RGB5_KY][3];
+    rgb5_load(p, n, oy, ox, valid, q);
+    f32x16 acc[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) acc[it] = f32x16{0};
+    auto ldw = [&](bf16x8 (&a)[IT], int g) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it) a[it] = lds_frag(rgb5_lds, ((g * IT + it) * 64 + lane) * 16);
+    };
+    bf16x8 fa[IT], fb[IT];
+    ldw(fa, 0);
+    auto step = [&](bf16x8 (&cur)[IT], bf16x8 (&nxt)[IT], int ky) __attribute__((always_inline)) {
+      if (ky + 1 < RGB5_KY) ldw(nxt, ky + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const f32x4 a = q[ky][0], bq = q[ky][1], c = q[ky][2];
+      const bf16x8 bs = {(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)bq[0], (__bf16)bq[1], (__bf16)bq[2],
+                         (__bf16)(h ? c[2] : c[0]), (__bf16)(h ? 0.f : c[1])};
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[it] = mfma32bf(cur[it], bs, acc[it]);
+    };
+#pragma unroll
+    for (int ky = 0; ky < RGB5_KY; ++ky) {
+      if (ky & 1) step(fb, fa, ky);
+      else step(fa, fb, ky);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    conv_epilogue<IT, EPI, 0, true, 0, true, 1>(p, acc, n, oy, ox, valid, 0, lp);
+  }
+}
+
 // GDN / IGDN backward (g_s.6 input gradient): 4 waves (one per SIMD: the wide epilogue needs the 512-register file),
 // each a sequence of row tiles; tile i's saved (y, s) loads are issued before its main loop and tile i+1's input
 // quads before tile i's epilogue, so their HBM latency hides behind MFMAs.  Every tile runs the same instruction
@@ -1950,7 +2013,7 @@ __global__ void pack_conv_x6w_kernel(const float* __restrict__ w, __bf16* __rest
 // dense tap-row fragments of conv_rgb5_x6, [cb][ky][it][lane][e] (three split planes): lane (h, r) supplies
 // A[r][k = 8 h + e] = W[o][c][ky][kx] with (kx, c) of the conv_rgb5_x6 K map (0 for c >= C and for h = 1, e = 7)
 __global__ void pack_conv_rgb5_x6_kernel(const float* __restrict__ w, __bf16* __restrict__ dst, int O, int C, long so,
-                                         long sc, int IT, long total) {
+                                         long sc, int IT, long total, int planes) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   long t = i;
@@ -1975,8 +2038,10 @@ __global__ void pack_conv_rgb5_x6_kernel(const float* __restrict__ w, __bf16* __
   const float r1 = v - (float)a;
   const __bf16 b = (__bf16)r1;
   dst[i] = a;
-  dst[total + i] = b;
-  dst[2 * total + i] = (__bf16)(r1 - (float)b);
+  if (planes == 3) {
+    dst[total + i] = b;
+    dst[2 * total + i] = (__bf16)(r1 - (float)b);
+  }
 }
 
 // the fp32 gamma' pack of ica_pack_gdn ([a][b][lane][r]) -> three bf16 planes [plane][a][b][s][lane][e], r = 8s + e
@@ -2244,6 +2309,23 @@ int launch_rgb_x6(const ConvParams& p, hipStream_t st) {
   return 0;
 }
 
+template <int EPI>
+int launch_rgb5_bf16(const ConvParams& p, hipStream_t st) {
+  const int total = ((p.Wout + 31) / 32) * p.Hout * p.N;
+  const int nblk = std::max(1, std::min(ica_cu_count(), (total + 7) / 8));
+  constexpr int lds = rgb5b_lds_bytes<EPI>();
+  static_assert(lds <= 160 * 1024, "conv_rgb5_bf16 LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_rgb5_bf16_kernel<EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  ICA_LAUNCH((conv_rgb5_bf16_kernel<EPI>), dim3(nblk), dim3(512), lds, st, p, nblk);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int IT, int EPI, int CG, int PT>
 int launch_up_x6_pt(const ConvParams& p, hipStream_t st) {
   const int tiles = ((p.Win + XU_TW - 1) / XU_TW) * ((p.Hin + xu_th<PT>() - 1) / xu_th<PT>()) * p.N;
@@ -2390,6 +2472,30 @@ int pick_up_x6(const ConvParams& p, hipStream_t st) {
 
 }  // namespace
 
+// bf16 RGB-side conv_down (ica_conv_ex prec = 1, kind 0, k5 s2, Cin <= 3, 128 outputs, plain fill, row-major input;
+// ica_conv.hip routes here): conv_rgb5_bf16_kernel on the order-2 pack of ica_pack_conv_weight_bf16
+int ica_rgb5_bf16_dispatch(const ConvParams& p, int epi, hipStream_t st) {
+  if (p.Cin > 3 || p.Cout != 32 * RGB5_IT || (p.pl & PL_IN)) return -3;
+  if (p.Hout * 2 != p.Hin + (p.Hin & 1) || p.Wout * 2 != p.Win + (p.Win & 1)) return -2;
+  switch (epi) {
+    case EPI_BIAS: return launch_rgb5_bf16<EPI_BIAS>(p, st);
+    case EPI_GDN: return launch_rgb5_bf16<EPI_GDN>(p, st);
+    case EPI_IGDN_BWD: return launch_rgb5_bf16<EPI_IGDN_BWD>(p, st);
+    default: return -5;
+  }
+}
+
+// the dense tap-row pack in `planes` split planes (3: x6; 1: bf16 = the round-to-nearest hi plane)
+int ica_pack_rgb5_planes(const float* w, void* dst, int O, int C, long so, long sc, int it, int planes,
+                         hipStream_t st) {
+  if (C > 3 || C <= 0 || it <= 0 || (planes != 1 && planes != 3)) return -2;
+  const long t3 = rgb5_plane_frags(O, it) * 8;
+  ICA_LAUNCH(pack_conv_rgb5_x6_kernel, dim3((t3 + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
+             O, C, so, sc, it, t3, planes);
+  ICA_CHECK_LAUNCH();
+  return 0;
+}
+
 // x6 launches (ica_conv_ex with prec = 2): the k5 s2 conv (kind 0) and transposed conv (kind 1) layers of the
 // bmshj2018 transforms.  Returns -4 / -3 / -2 / -5 for shapes / epilogues without an x6 kernel: nothing falls back
 // here; hip_ops.x6_ok restates this coverage so that PackedConv keeps the fp32 pack for such layers.
@@ -2470,11 +2576,7 @@ int ica_pack_conv_weight_x6(const float* w, void* dst, int O, int C, int KS, lon
   if (it <= 0) return -3;
   if (order == 2) {
     if (KS != 5 || C > 3 || C <= 0) return -2;
-    const long t3 = rgb5_plane_frags(O, it) * 8;
-    ICA_LAUNCH(pack_conv_rgb5_x6_kernel, dim3((t3 + 255) / 256), dim3(256), 0, st, w, reinterpret_cast<__bf16*>(dst),
-               O, C, so, sc, it, t3);
-    ICA_CHECK_LAUNCH();
-    return 0;
+    return ica_pack_rgb5_planes(w, dst, O, C, so, sc, it, 3, st);
   }
   if (order != 0 && order != 1) return -2;
   const long total = x6_plane_frags(O, C, KS, it) * 8;

@@ -265,7 +265,11 @@ class PackedConv:
             self.Cout, self.Cin = weight.shape[0], weight.shape[1]
             # forward: o = co, c = ci
             if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cin >= 16 or self.Cin <= 4):
-                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK, ORDER_DOWN, it=it_fwd)
+                # an RGB input into 128 channels: the dense tap-row pack of conv_rgb5_bf16 (ica_conv_ex routes those
+                # launches there); other shapes keep the tap groups / 16-channel chunks
+                rgb5 = self.Cin <= 3 and self.Cout == 128 and it_fwd in (0, 4)
+                self.fwd = pack_conv_bf16(weight, self.Cout, self.Cin, 5, self.Cin * KK, KK,
+                                          ORDER_RGB5 if rgb5 else ORDER_DOWN, it=it_fwd)
                 self.fwd_prec = PREC_BF16
             else:
                 self.fwd = pack_conv(weight, self.Cout, self.Cin, self.KS, self.Cin * KK, KK, ORDER_DOWN,
@@ -299,7 +303,9 @@ class PackedConv:
                                      it=it_fwd)
             # dgrad (conv_down, stride 2): o = ci, c = co
             if prec == PREC_BF16 and self.KS == 5 and stride == 2 and (self.Cout >= 16 or self.Cout <= 4):
-                self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK, ORDER_DOWN, it=it_bwd)
+                rgb5 = self.Cout <= 3 and self.Cin == 128 and it_bwd in (0, 4)
+                self.bwd = pack_conv_bf16(weight, self.Cin, self.Cout, 5, self.Cout * KK, KK,
+                                          ORDER_RGB5 if rgb5 else ORDER_DOWN, it=it_bwd)
                 self.bwd_prec = PREC_BF16
             else:
                 self.bwd = pack_conv(weight, self.Cin, self.Cout, self.KS, self.Cout * KK, KK, ORDER_DOWN,
