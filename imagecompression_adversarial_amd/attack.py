@@ -193,8 +193,10 @@ class AttackLoop:
         # wall time spent blocked in those waits (bench.py --mixed reports them)
         self.sync_steps = 0
         self.sync_wait_s = 0.0
-        # the whole-batch network step as a HIP graph (L2 losses; the ms-ssim loss path and the ROI attack run eager)
-        self.graph_ok = ATTACK_GRAPH and dev.type == "cuda" and att_metric == "L2" and target is None
+        # the whole-batch network step as a HIP graph (L2 losses; the ms-ssim loss path, the ROI attack and subclasses
+        # with their own network step -- the defended attack's, which reads its variant choice on the host -- run eager)
+        self.graph_ok = (ATTACK_GRAPH and dev.type == "cuda" and att_metric == "L2" and target is None
+                         and type(self).network_grad is AttackLoop.network_grad)
         self._graph, self._graph_out = None, None
         self.graph_replays = 0
         # pre-eval: output_s, bpp_ori (attack_rd.py:401-419)
