@@ -308,10 +308,6 @@ def bench_finetune(args):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    K.EVENT_HOOK = {}
-    K.FLOPS_HOOK = {}
-    K.PREC_HOOK = {}
-    K.LAUNCH_HOOK = {}
     D.COLL_HOOK = {} if dist else None
     from imagecompression_adversarial_amd import attack as A
     g0 = dict(A.GRAPH_STATS)
@@ -325,6 +321,21 @@ def bench_finetune(args):
     coll, D.COLL_HOOK = D.COLL_HOOK, None
     # all-reduce time per outer step (HIP events around each collective on the issuing stream)
     coll_ms = {k: sum(a.elapsed_time(b) for a, b in v) / args.steps for k, v in (coll or {}).items()}
+    replays = A.GRAPH_STATS["replays"] - g0["replays"]
+    captures = A.GRAPH_STATS["captures"] - g0["captures"]
+    # Per-kernel times: the timed outer steps replay the inner attack's network step as a HIP graph (one launch per
+    # inner step; its kernels carry no events), so ONE more outer step runs right after them with the graph off and
+    # every tagged launch bracketed by HIP events: per-launch times, launch counts and the launch table of a whole
+    # outer step (the roofline and the PMC stamps refer to these launches, which run the same kernels on the same
+    # shapes as the replays).
+    graph_on, A.ATTACK_GRAPH = A.ATTACK_GRAPH, False
+    K.EVENT_HOOK = {}
+    K.FLOPS_HOOK = {}
+    K.PREC_HOOK = {}
+    K.LAUNCH_HOOK = {}
+    adv_step(net, tr, opt, aux, xs[args.warmup], fargs, group, world)
+    torch.cuda.synchronize()
+    A.ATTACK_GRAPH = graph_on
     hook, K.EVENT_HOOK = K.EVENT_HOOK, None
     table = _launch_table(K.LAUNCH_HOOK, rank)
     K.LAUNCH_HOOK = None
@@ -335,14 +346,8 @@ def bench_finetune(args):
         el = float(t.item())
     N, M = net.N, net.M
     flops_img = {t: (K.FLOPS_HOOK[t] if t in K.FLOPS_HOOK else layer_flops(t, N, M, H, W, 1)) for t in hook}
-    tot_ms, tot_fl = _kernel_table(hook, flops_img)
-    # the inner attack's whole-batch network steps replay a HIP graph (attack.AttackLoop._network_graph): the event
-    # hooks time the eager launches only (the first step of each inner attack, and the train step), so a network tag's
-    # launches per outer step are its eager ones plus one per replay, each at the eager per-launch mean
-    replays = A.GRAPH_STATS["replays"] - g0["replays"]
-    captures = A.GRAPH_STATS["captures"] - g0["captures"]
-    net_tag = lambda t: "[" not in t and t.rsplit(".", 1)[-1] in ("fwd", "dgrad")   # noqa: E731
-    est_ms = {t: tot_ms[t] / len(hook[t]) * (len(hook[t]) + (replays if net_tag(t) else 0)) for t in tot_ms}
+    tot_ms, tot_fl = _kernel_table(hook, flops_img)   # one eager outer step
+    est_ms = dict(tot_ms)
     dom = max(est_ms, key=est_ms.get)
     wg = [t for t in tot_ms if t.endswith(".wgrad")]
     wdom = max(wg, key=tot_ms.get) if wg else None
@@ -379,10 +384,11 @@ def bench_finetune(args):
                                            "rank_extra_is": "flat-gradient all-reduce ms per outer step"}
                                           if dist else {})),
             "roofline": roof(dom), "wgrad_roofline": roof(wdom),
-            "per_kernel_ms_total_per_outer_step": {k: round(v / args.steps, 3) for k, v in sorted(est_ms.items())},
+            "per_kernel_ms_total_per_outer_step": {k: round(v, 3) for k, v in sorted(est_ms.items())},
             "attack_graph": {"captures_per_outer_step": round(captures / args.steps, 3),
                              "replays_per_outer_step": round(replays / args.steps, 3),
-                             "note": "network tags: eager per-launch mean x (eager launches + graph replays)"},
+                             "note": "timed steps replay the inner network step as a HIP graph; per-kernel times, "
+                                     "roofline and launch table from one eager outer step run after them"},
             "cpu_baseline": (None if world > 1 or args.no_cpu_baseline else
                              cpu_baseline_finetune(q, metric, lmbda, B, H, W, inner)),
         }
