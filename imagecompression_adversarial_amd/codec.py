@@ -907,7 +907,8 @@ class DebugHyperSynthesisTransform(MbtHyperSynthesisTransform):
 class AeOneLayer(CompressionModel):
     """anchors/model.py:8-33 ae_onelayer(MeanScaleHyperprior): one 3x3 stride-1 conv each way around the mean-scale
     hyperprior; forward reconstructs from the unquantised latent.  No pretrained weights exist (anchors/model.py:62):
-    random / user-supplied weights, eval forward and the attack path (fp32 operands)."""
+    random / user-supplied weights, eval forward, the attack path (fp32 operands), the train-mode forward's values;
+    the fine-tune's gradients come from train_engine.RDTrainer -> train_debug.DebugTrainStep."""
     model_kind = "debug"
 
     def __init__(self, N=3, M=192, **kwargs):
@@ -925,7 +926,8 @@ class AeOneLayer(CompressionModel):
 
     def forward(self, x):
         if self.training:
-            raise NotImplementedError("ae_onelayer training is out of scope on the HIP path (eval forward only)")
+            from .train_debug import train_forward
+            return _train_values(self, x, train_forward)
         res = self.kernels("fp32").forward(K.to_nc4(x.detach().contiguous()))
         return {"x_hat": K.from_nc4(res["x_hat4"], 3),
                 "likelihoods": {"y": K.from_nc4(res["lik4"]["y"], self.M), "z": K.from_nc4(res["lik4"]["z"], self.N)}}

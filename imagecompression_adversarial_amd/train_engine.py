@@ -113,10 +113,10 @@ class RDTrainer:
             raise ValueError(f"metric {metric!r}: the HIP trainer supports mse and ms-ssim (lpips is out of scope)")
         self.net, self.metric, self.lmbda = net, metric, float(lmbda)
         self.kind = net.model_kind
-        if self.kind not in ("factorized", "hyper", "cheng2020", "context"):
-            raise NotImplementedError(f"the HIP trainer covers bmshj2018, mbt2018 and cheng2020-anchor, not "
-                                      f"{self.kind!r}")
-        self._joint = None   # cheng2020 / mbt2018 (train_cheng, train_mbt)
+        if self.kind not in ("factorized", "hyper", "cheng2020", "context", "debug"):
+            raise NotImplementedError(f"the HIP trainer covers bmshj2018, mbt2018, cheng2020-anchor and the debug "
+                                      f"model, not {self.kind!r}")
+        self._joint = None   # cheng2020 / mbt2018 / ae_onelayer (train_cheng, train_mbt, train_debug)
         # train.py:77-83: lambda == 100 is the reference's "Inf mode", the rate term leaves the loss (lamb_r = 0)
         self.lamb_r = 0.0 if self.lmbda == 100 else 1.0
         if self.lamb_r == 0.0:
@@ -183,10 +183,12 @@ class RDTrainer:
         """One train-mode forward + loss + backward.  x: [B,3,H,W] on the device (H, W multiples of 64).
         noise_y / noise_z: optional NCHW U(-1/2,1/2) quantisation noise (drawn here when None).
         Returns {"loss", "bpp_loss", "distortion_loss"} as 0-d device tensors; grads in p.grad."""
-        if self.kind in ("cheng2020", "context"):
+        if self.kind in ("cheng2020", "context", "debug"):
             if self._joint is None:
                 if self.kind == "cheng2020":
                     from .train_cheng import ChengTrainStep as Step
+                elif self.kind == "debug":
+                    from .train_debug import DebugTrainStep as Step
                 else:
                     from .train_mbt import MbtTrainStep as Step
                 self._joint = Step(self)
