@@ -143,11 +143,11 @@ def _tag_prec(kern):
     return out
 
 
-_PREC_NAME = {0: "fp32", 1: "bf16", 2: "x6"}
+_PREC_NAME = {0: "fp32", 1: "bf16", 2: "x6", 3: "bf16 (fp32 activations)"}
 
 
 def _peak(prec):
-    return {1: BF16_MFMA_PEAK_TFLOPS, 2: X6_PEAK_TFLOPS}.get(prec, FP32_MFMA_PEAK_TFLOPS)
+    return {1: BF16_MFMA_PEAK_TFLOPS, 2: X6_PEAK_TFLOPS, 3: BF16_MFMA_PEAK_TFLOPS}.get(prec, FP32_MFMA_PEAK_TFLOPS)
 
 
 def _dist_env():

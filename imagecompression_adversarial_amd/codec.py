@@ -654,13 +654,15 @@ class CompressionModel(nn.Module):
 
     def attack_precision(self, requested: str | None = None) -> str:
         """Conv operand precision of the attack engine: the request, else x6 (fp32-accurate bf16x6): the 5x5
-        stride-2 transforms of bmshj2018 / mbt2018, and cheng2020's 3x3 stride-1 residual convs (its strided,
-        subpel-gradient and RGB convs keep fp32 operands)."""
+        stride-2 transforms of bmshj2018 / mbt2018, and cheng2020's 3x3 convs (engine_cheng.ChengKernels lists which
+        launches; the rest keep fp32 operands).  'bf16': bf16-operand convs (bmshj2018 / mbt2018: bf16 activations
+        too; cheng2020: bf16 operands over fp32 activations on its k3 conv_downs)."""
         return requested or "x6"
 
     def kernels(self, precision: str = "fp32"):
         """Whole-model HIP executor (used by the attack engine).  precision 'bf16': bf16-operand g_a / g_s
-        convs (bmshj2018 models; BASELINE config 5).  One executor per precision, each valid for one weight
+        convs (bmshj2018 / mbt2018: BASELINE config 5; cheng2020: engine_cheng.ChengKernels).  One executor per
+        precision, each valid for one weight
         version: the fine-tune's x6 inner attack and fp32 train step share a weight update without repacking
         each other's executor (train.py adv_step -> RDTrainer.step)."""
         key = tuple((p.data_ptr(), p._version) for p in self.parameters())
@@ -672,8 +674,6 @@ class CompressionModel(nn.Module):
         if ex is None:
             sd = {k: v.detach() for k, v in self.state_dict().items()}
             if self.model_kind == "cheng2020":
-                if precision not in ("fp32", "x6"):
-                    raise NotImplementedError("the bf16 conv path covers the bmshj2018 transforms")
                 ex = EC.ChengKernels(sd, precision=precision)
             elif self.model_kind == "debug":
                 ex = ED.DebugKernels(sd, precision=precision)

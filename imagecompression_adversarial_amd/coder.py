@@ -207,8 +207,8 @@ def config():
     p.add_argument("--batch", dest="batch", type=int, default=1,
                    help="attack this many same-size images per launch (per-image semantics preserved)")
     p.add_argument("--precision", dest="precision", type=str, default=None, choices=("x6", "fp32", "bf16"),
-                   help="g_a/g_s conv operands: x6 (default for the bmshj2018 / mbt2018 models: fp32-accurate "
-                        "bf16x6 split-operand MFMA, error vs float64 no larger than the fp32-operand path's), fp32 "
-                        "(fp32-operand MFMA; the cheng2020 default) or bf16 (bf16 operands, fp32 accumulate; "
-                        "BASELINE config 5)")
+                   help="g_a/g_s conv operands: x6 (the default: fp32-accurate bf16x6 split-operand MFMA, error "
+                        "vs float64 no larger than the fp32-operand path's), fp32 (fp32-operand MFMA; the debug "
+                        "model's only one) or bf16 (bf16 operands, fp32 accumulate; BASELINE config 5; cheng2020: "
+                        "over fp32 activations)")
     return p

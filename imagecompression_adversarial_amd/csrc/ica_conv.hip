@@ -87,7 +87,10 @@ constexpr int conv_down_waves() {
 // ica_pack_gdn_x6 pack): the k3 s1 layers of cheng2020 on the x6 ceiling.  One block per CU (512 registers); two for
 // IT = 1 (g_s.7's 16 rho rows: 16 accumulators).
 // XPT: 32-px rows per wave on the X6O path (2 at IT >= 4 on large grids, see pick_tw_down_x6o).
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1>
+// NPL: bf16 planes of the X6O operands: 3 = x6 (six MFMAs per k step); 1 = bf16 operands over fp32 activations
+// (ICA_PREC_B1: the hi plane alone, i.e. RNE bf16 of the activations and of the weights, one MFMA per k step, fp32
+// accumulate; the GDN epilogue GEMMs stay x6) -- cheng2020's --precision bf16.
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1, int NPL = 3>
 __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS, IT, CC, EPI, BF>())) void conv_down_kernel(ConvParams p) {
   constexpr int PT = X6O ? XPT : down_pt<CC, BF>();
   static_assert(XPT == 1 || (X6O && XPT == 2 && (ICA_X6O_PT2_GDN || !epi_gdn<EPI>()) && IT >= 4), "x6 conv_down: two rows per wave at IT >= 4");
@@ -101,6 +104,7 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
   // bf16 with CC == 4 (an RGB conv input): K = 4 taps x 4 channels per MFMA ("tap groups"), fp32 LDS patch
   static_assert(!BF || CC == 16 || CC == 4, "bf16 conv_down: 16-channel chunks or 4-channel tap groups");
   static_assert(!X6O || (!BF && CC == 16), "x6 conv_down: fp32 fills of 16-channel chunks");
+  static_assert(NPL == 3 || (NPL == 1 && X6O), "one-plane operands: the X6O kernel only");
   // X6O: [buffer][plane][half][pixel], 8 channels as bf16; the GDN-backward epilogues park g*s in it afterwards
   // (IT*16 floats per lane, one slab per wave)
   constexpr bool XST = X6O && (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) && !(FX == 0 && IT <= 4);
@@ -469,7 +473,7 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
 #pragma unroll
       for (int it = 0; it < IT; ++it)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
+        for (int q = 0; q < NPL; ++q) a[it][q] = ld_bf8(wr, lane * 16, (int)((q * ps + f + it * 64) * 16));
     };
     // Double-buffered patch (X6DB): chunk c + 1 is staged into the other 6-plane buffer while chunk c's taps run
     // -- its NF quads per thread are issued one per tap (taps 0..NF-1, after that tap's weight prefetch) and split
@@ -528,8 +532,10 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
         u32x2* p2 = reinterpret_cast<u32x2*>(buf);
         const int ent = (q >> 1) * PLANE + pix;
         p2[(0 * 2 * PLANE + ent) * 2 + (q & 1)] = a;
-        p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
-        p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+        if constexpr (NPL == 3) {
+          p2[(1 * 2 * PLANE + ent) * 2 + (q & 1)] = b;
+          p2[(2 * 2 * PLANE + ent) * 2 + (q & 1)] = c;
+        }
       }
     };
 #pragma unroll
@@ -559,8 +565,10 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
           for (int t = 0; t < PT; ++t) {
             const int o = h * PLANE + lb[t] + ky * PC + kx;
             b[t][0] = f4_as_bf8(cur[o]);
-            b[t][1] = f4_as_bf8(cur[2 * PLANE + o]);
-            b[t][2] = f4_as_bf8(cur[4 * PLANE + o]);
+            if constexpr (NPL == 3) {
+              b[t][1] = f4_as_bf8(cur[2 * PLANE + o]);
+              b[t][2] = f4_as_bf8(cur[4 * PLANE + o]);
+            }
           }
         };
         ldb(bb[0], 0);
@@ -577,7 +585,7 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
           for (int it = 0; it < IT; ++it)
 #pragma unroll
             for (int t = 0; t < PT; ++t)
-              acc[t][it] = mfma_x6(fr[(R0 + tap) & 1][it], bb[tap & 1][t], acc[t][it]);
+              acc[t][it] = mfma_np<NPL>(fr[(R0 + tap) & 1][it], bb[tap & 1][t], acc[t][it]);
         }
         __syncthreads();
       };
@@ -604,8 +612,10 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
           const int ky = tap / KS, kx = tap - (tap / KS) * KS;
           const int o = h * PLANE + lbase + ky * PC + kx;
           b[0] = f4_as_bf8(cur[o]);
-          b[1] = f4_as_bf8(cur[2 * PLANE + o]);
-          b[2] = f4_as_bf8(cur[4 * PLANE + o]);
+          if constexpr (NPL == 3) {
+            b[1] = f4_as_bf8(cur[2 * PLANE + o]);
+            b[2] = f4_as_bf8(cur[4 * PLANE + o]);
+          }
         };
         ldb(bb[0], 0);
   #pragma unroll
@@ -619,7 +629,7 @@ __global__ __launch_bounds__(256, X6O ? (IT == 1 ? 2 : 1) : (conv_down_waves<KS,
           if (tap + 1 < KK) ldb(bb[(tap + 1) & 1], tap + 1);
           __builtin_amdgcn_sched_barrier(0);
   #pragma unroll
-          for (int it = 0; it < IT; ++it) acc[0][it] = mfma_x6(fr[tap % 3][it], bb[tap & 1], acc[0][it]);
+          for (int it = 0; it < IT; ++it) acc[0][it] = mfma_np<NPL>(fr[tap % 3][it], bb[tap & 1], acc[0][it]);
         }
         __syncthreads();
       }
@@ -1783,12 +1793,12 @@ constexpr bool down_variant() {
 template <int KS, int S>
 constexpr bool down_cc4() { return (KS == 5 && S == 2) || (KS == 3 && S == 2) || (KS == 1 && S == 2); }
 
-template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1>
+template <int KS, int S, int IT, int CC, int TW, int EPI, int FX, bool BF, bool X6O = false, int XPT = 1, int NPL = 3>
 static int launch_down(const ConvParams& p, hipStream_t st) {
   constexpr int TH = (X6O ? XPT : down_pt<CC, BF>()) * 128 / TW;
   const int tiles = ((p.Wout + TW - 1) / TW) * ((p.Hout + TH - 1) / TH) * p.N;
   dim3 grid(tiles, (p.Cout + IT * 32 - 1) / (IT * 32));
-  ICA_LAUNCH((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O, XPT>), grid, dim3(256), 0, st, p);
+  ICA_LAUNCH((conv_down_kernel<KS, S, IT, CC, TW, EPI, FX, BF, X6O, XPT, NPL>), grid, dim3(256), 0, st, p);
   ICA_CHECK_LAUNCH();
   return 0;
 }
@@ -1796,7 +1806,7 @@ static int launch_down(const ConvParams& p, hipStream_t st) {
 // x6 operands for the k3 s1 conv_downs (cheng2020 g_a / g_s and their input gradients): plain, leaky-ReLU-mask and
 // PixelUnshuffle fills with the residual / PixelShuffle extras, IT 4 / 6; the t output (FX_T) and other extras
 // return -4 (nothing falls back here: engine_cheng._x6_ok keeps the fp32 pack for launches writing t)
-template <int IT, int EPI, int FX>
+template <int IT, int EPI, int FX, int NPL>
 static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
   if constexpr (!down_variant<3, 1, IT, EPI, FX>()) {
     return -4;
@@ -1808,64 +1818,75 @@ static int pick_tw_down_x6o(const ConvParams& p, hipStream_t st) {
       const int cbs = (p.Cout + IT * 32 - 1) / (IT * 32);
       if (p.Wout >= 32 && p.Wout % 32 == 0) {
         if ((long)(p.Wout / 32) * ((p.Hout + 7) / 8) * p.N * cbs >= 1024)
-          return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true, 2>(p, st);
+          return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true, 2, NPL>(p, st);
       } else if ((long)((p.Wout + 15) / 16) * ((p.Hout + 15) / 16) * p.N * cbs >= 1024) {
-        return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true, 2>(p, st);
+        return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true, 2, NPL>(p, st);
       }
     }
-    if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true>(p, st);
-    return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true>(p, st);
+    if (p.Wout >= 32 && p.Wout % 32 == 0) return launch_down<3, 1, IT, 16, 32, EPI, FX, false, true, 1, NPL>(p, st);
+    return launch_down<3, 1, IT, 16, 16, EPI, FX, false, true, 1, NPL>(p, st);
   }
 }
 // x6 operands for the k3 s2 forwards (cheng2020 g_a.2 / g_a.4 conv1: leaky ReLU, and bias): one row per wave, the
 // fill two quads per tap
-template <int IT>
+template <int IT, int NPL>
 static int pick_down_x6o_s2(const ConvParams& p, int epi, int fx, hipStream_t st) {
   if (fx != 0) return -4;
   const bool w32 = p.Wout >= 32 && p.Wout % 32 == 0;
   if (epi == EPI_LRELU)
-    return w32 ? launch_down<3, 2, IT, 16, 32, EPI_LRELU, 0, false, true>(p, st)
-               : launch_down<3, 2, IT, 16, 16, EPI_LRELU, 0, false, true>(p, st);
+    return w32 ? launch_down<3, 2, IT, 16, 32, EPI_LRELU, 0, false, true, 1, NPL>(p, st)
+               : launch_down<3, 2, IT, 16, 16, EPI_LRELU, 0, false, true, 1, NPL>(p, st);
   if (epi == EPI_BIAS)
-    return w32 ? launch_down<3, 2, IT, 16, 32, EPI_BIAS, 0, false, true>(p, st)
-               : launch_down<3, 2, IT, 16, 16, EPI_BIAS, 0, false, true>(p, st);
+    return w32 ? launch_down<3, 2, IT, 16, 32, EPI_BIAS, 0, false, true, 1, NPL>(p, st)
+               : launch_down<3, 2, IT, 16, 16, EPI_BIAS, 0, false, true, 1, NPL>(p, st);
   return -4;
 }
-template <int IT, int EPI>
+template <int IT, int EPI, int NPL>
 static int pick_fx_down_x6o(const ConvParams& p, int fx, hipStream_t st) {
   switch (fx) {
-    case 0: return pick_tw_down_x6o<IT, EPI, 0>(p, st);
-    case FX_RES: return pick_tw_down_x6o<IT, EPI, FX_RES>(p, st);
-    case FX_PS: return pick_tw_down_x6o<IT, EPI, FX_PS>(p, st);
-    case FX_MASK: return pick_tw_down_x6o<IT, EPI, FX_MASK>(p, st);
-    case FX_UNSHUF: return pick_tw_down_x6o<IT, EPI, FX_UNSHUF>(p, st);
-    case FX_UNSHUF | FX_RES: return pick_tw_down_x6o<IT, EPI, FX_UNSHUF | FX_RES>(p, st);
+    case 0: return pick_tw_down_x6o<IT, EPI, 0, NPL>(p, st);
+    case FX_RES: return pick_tw_down_x6o<IT, EPI, FX_RES, NPL>(p, st);
+    case FX_PS: return pick_tw_down_x6o<IT, EPI, FX_PS, NPL>(p, st);
+    case FX_MASK: return pick_tw_down_x6o<IT, EPI, FX_MASK, NPL>(p, st);
+    case FX_UNSHUF: return pick_tw_down_x6o<IT, EPI, FX_UNSHUF, NPL>(p, st);
+    case FX_UNSHUF | FX_RES: return pick_tw_down_x6o<IT, EPI, FX_UNSHUF | FX_RES, NPL>(p, st);
     default: return -4;
   }
 }
-template <int IT>
+template <int IT, int NPL>
 static int pick_epi_down_x6o(const ConvParams& p, int epi, int fx, hipStream_t st) {
   switch (epi) {
-    case EPI_BIAS: return pick_fx_down_x6o<IT, EPI_BIAS>(p, fx, st);
-    case EPI_RELU: return pick_fx_down_x6o<IT, EPI_RELU>(p, fx, st);
-    case EPI_LRELU: return pick_fx_down_x6o<IT, EPI_LRELU>(p, fx, st);
-    case EPI_LRELU_BWD: return pick_fx_down_x6o<IT, EPI_LRELU_BWD>(p, fx, st);
-    case EPI_GDN: return pick_fx_down_x6o<IT, EPI_GDN>(p, fx, st);
-    case EPI_IGDN: return pick_fx_down_x6o<IT, EPI_IGDN>(p, fx, st);
-    case EPI_GDN_BWD: return pick_fx_down_x6o<IT, EPI_GDN_BWD>(p, fx, st);
-    case EPI_IGDN_BWD: return pick_fx_down_x6o<IT, EPI_IGDN_BWD>(p, fx, st);
+    case EPI_BIAS: return pick_fx_down_x6o<IT, EPI_BIAS, NPL>(p, fx, st);
+    case EPI_RELU: return pick_fx_down_x6o<IT, EPI_RELU, NPL>(p, fx, st);
+    case EPI_LRELU: return pick_fx_down_x6o<IT, EPI_LRELU, NPL>(p, fx, st);
+    case EPI_LRELU_BWD: return pick_fx_down_x6o<IT, EPI_LRELU_BWD, NPL>(p, fx, st);
+    case EPI_GDN: return pick_fx_down_x6o<IT, EPI_GDN, NPL>(p, fx, st);
+    case EPI_IGDN: return pick_fx_down_x6o<IT, EPI_IGDN, NPL>(p, fx, st);
+    case EPI_GDN_BWD: return pick_fx_down_x6o<IT, EPI_GDN_BWD, NPL>(p, fx, st);
+    case EPI_IGDN_BWD: return pick_fx_down_x6o<IT, EPI_IGDN_BWD, NPL>(p, fx, st);
     default: return -5;
   }
 }
+template <int NPL>
 static int pick_down_x6o(const ConvParams& p, int it, int epi, int fx, hipStream_t st) {
   if (p.Cin < 16) return -4;
   switch (it) {
     case 1:   // cheng2020 g_s.7, subpel_conv3x3(N, 3, 2): 16 rho rows, PixelShuffle store
-      return epi == EPI_BIAS && fx == FX_PS ? pick_tw_down_x6o<1, EPI_BIAS, FX_PS>(p, st) : -4;
-    case 4: return pick_epi_down_x6o<4>(p, epi, fx, st);
-    case 6: return pick_epi_down_x6o<6>(p, epi, fx, st);
+      return epi == EPI_BIAS && fx == FX_PS ? pick_tw_down_x6o<1, EPI_BIAS, FX_PS, NPL>(p, st) : -4;
+    case 4: return pick_epi_down_x6o<4, NPL>(p, epi, fx, st);
+    case 6: return pick_epi_down_x6o<6, NPL>(p, epi, fx, st);
     default: return -4;
   }
+}
+// the k3 conv_downs on X6O operands: NPL = 3 (x6) or 1 (ICA_PREC_B1)
+template <int NPL>
+static int pick_x6o(const ConvParams& p, int kind, int KS, int S, int epi, int it, int fx, hipStream_t st) {
+  if (kind == 0 && KS == 3 && S == 1) return pick_down_x6o<NPL>(p, it, epi, fx, st);
+  if (kind == 0 && KS == 3 && S == 2 && p.fill_mode == 0 && !p.ps) {
+    if (it == 6) return pick_down_x6o_s2<6, NPL>(p, epi, fx, st);
+    if (it == 4) return pick_down_x6o_s2<4, NPL>(p, epi, fx, st);
+  }
+  return -4;
 }
 
 // small-grid variant (conv_down_split_kernel): outputs of at most 64 x 64 pixels per image.  A per-image
@@ -2410,7 +2431,7 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   ConvParams p{a->x,    a->y,    a->wp,   a->bias, a->gp,   a->beta, a->save_x, a->save_s, a->in_x, a->in_s,
                a->N,    a->Cin,  a->Hin,  a->Win,  a->Cout, a->Hout, a->Wout,   a->save_t, a->res,  a->mask,
                a->fill_mode, a->ps, a->prec, a->layout};
-  if (a->prec != 0 && a->prec != 1 && a->prec != 2) return -4;
+  if (a->prec < 0 || a->prec > 3) return -4;
   // parity-split tensors: the k5 s2 layers of the bmshj2018 transforms (plain fill, no PixelShuffle), even planes
   if (a->layout & ~(PL_IN | PL_OUT)) return -4;
   if (a->layout && (a->KS != 5 || a->S != 2 || a->fill_mode != 0 || a->ps)) return -4;
@@ -2425,14 +2446,11 @@ int ica_conv_ex(const ica_conv_args* a, hipStream_t st) {
   const int fx = ((a->res || a->save_x) ? FX_RES : 0) | (a->ps ? FX_PS : 0) | (a->fill_mode == 1 ? FX_MASK : 0) |
                  (a->fill_mode == 2 ? FX_UNSHUF : 0) | (a->save_t ? FX_T : 0);
   if (a->prec == 2) {
-    if (a->kind == 0 && a->KS == 3 && a->S == 1) return pick_down_x6o(p, it, a->epi, fx, st);
-    if (a->kind == 0 && a->KS == 3 && a->S == 2 && a->fill_mode == 0 && !a->ps) {
-      if (it == 6) return pick_down_x6o_s2<6>(p, a->epi, fx, st);
-      if (it == 4) return pick_down_x6o_s2<4>(p, a->epi, fx, st);
-      return -4;
-    }
+    if (a->kind == 0 && a->KS == 3) return pick_x6o<3>(p, a->kind, a->KS, a->S, a->epi, it, fx, st);
     return ica_conv_x6_dispatch(p, a->kind, a->KS, a->S, it, a->epi, fx, st);
   }
+  // bf16 operands over fp32 activations: the k3 conv_downs only, on the x6 pack's hi plane (cheng2020 bf16)
+  if (a->prec == 3) return pick_x6o<1>(p, a->kind, a->KS, a->S, a->epi, it, fx, st);
   // bf16 RGB-side conv_down with the dense tap-row pack (hip_ops packs order 2 for exactly these layers)
   if (a->prec == 1 && a->kind == 0 && a->KS == 5 && a->S == 2 && a->Cin <= 3 && a->Cout == 128 && it == 4 && fx == 0 &&
       a->fill_mode == 0 && (a->epi == EPI_BIAS || a->epi == EPI_GDN || a->epi == EPI_IGDN_BWD))

@@ -87,6 +87,12 @@ ICA_DEV f32x16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
   c = mfma32bf(a[0], b[0], c);
   return c;
 }
+// NPL planes: 3 = the six x6 products; 1 = the hi planes alone (bf16 operands, RNE)
+template <int NPL>
+ICA_DEV f32x16 mfma_np(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  if constexpr (NPL == 1) return mfma32bf(a[0], b[0], c);
+  else return mfma_x6(a, b, c);
+}
 
 // channels c0..c0+3 of a per-channel vector (bias, beta'): one 16-B buffer load, no branch.  A null vector gets a
 // zero-range descriptor and reads 0; the range is rounded up to whole quads (a quad that straddles C is read whole,

@@ -34,7 +34,9 @@ def _k(prefix, name):
 
 
 def _it(C):
-    return 6 if C == 192 else (1 if C <= 32 else 0)
+    """32-channel row tiles per wave: 6 for N = 192 (q4-6), 4 for N = 128 (q1-3; explicit, so the x6 / bf16 packs
+    below are built for it too), 1 for the 3- and 16-row layers, else the library default."""
+    return 6 if C == 192 else (4 if C == 128 else (1 if C <= 32 else 0))
 
 
 def rho_perm(C: int, device) -> torch.Tensor:
@@ -67,8 +69,12 @@ X6_IT_PS = (1, 4, 6)   # ... and of the subpel forwards (IT = 1: g_s.7's 16 rho 
 class Conv3:
     """One Conv2d(k in {1,3,5}, stride s, pad k//2) layer, packed for its forward and its input gradient."""
 
-    def __init__(self, w, b, stride=1, fwd_only=False, mask=None, x6=False):
+    def __init__(self, w, b, stride=1, fwd_only=False, mask=None, x6=False, b1=False):
+        """b1 (with x6): the X6O conv_down launches (k3 s1 forward / input gradient, k3 s2 forward) run bf16
+        operands over fp32 activations (hip_ops.PREC_B1: the x6 pack's hi plane); the stride-2 input gradients keep
+        x6 (cheng2020 --precision bf16)."""
         w = w.detach()
+        self.p6 = K.PREC_B1 if b1 else K.PREC_X6
         if mask is not None:
             w = (w * mask.to(w.device)).contiguous()
         self.Cout, self.Cin, self.KS = w.shape[0], w.shape[1], w.shape[-1]
@@ -107,14 +113,14 @@ class Conv3:
     def forward(self, x4, epi=K.EPI_BIAS, **kw):
         if self.fwd6 is not None and _x6_ok(kw):
             return K.conv_ex(x4, self.Cin, self.fwd6, self.bias, self.Cout, self.KS, self.S, 0, epi, self.it,
-                             prec=K.PREC_X6, **kw)
+                             prec=self.p6, **kw)
         return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.Cout, self.KS, self.S, 0, epi, self.it, **kw)
 
     def dgrad(self, g4, epi=K.EPI_BIAS, **kw):
         if self.S == 1:
             if self.bwd6 is not None and _x6_ok(kw):
                 return K.conv_ex(g4, self.Cout, self.bwd6, None, self.Cin, self.KS, 1, 0, epi, self.it_b,
-                                 prec=K.PREC_X6, **kw)
+                                 prec=self.p6, **kw)
             return K.conv_ex(g4, self.Cout, self.bwd, None, self.Cin, self.KS, 1, 0, epi, self.it_b, **kw)
         if self.bwd6 is not None and epi == K.EPI_BIAS and _x6_ok(kw):
             return K.conv_ex(g4, self.Cout, self.bwd6, None, self.Cin, self.KS, 2, 1, epi, self.it_b,
@@ -131,12 +137,13 @@ def _x6_ok(kw):
 class Subpel:
     """subpel_conv3x3(Cin, C, 2) = Conv2d(Cin, 4C, 3, p=1) + PixelShuffle(2), rho-ordered rows."""
 
-    def __init__(self, w, b, fwd_only=False, x6=False):
+    def __init__(self, w, b, fwd_only=False, x6=False, b1=False):
+        self.p6 = K.PREC_B1 if b1 else K.PREC_X6   # as Conv3
         self.C = w.shape[0] // 4
         self.Cin = w.shape[1]
         wr, self.bias = _rho_weight(w, b, self.C)
         self.R = wr.shape[0]          # rho rows = 16 * ceil(C / 4)
-        self.it = _it(self.R) if self.R != 768 else 6
+        self.it = 6 if self.R == 768 else (4 if self.R % 128 == 0 else _it(self.R))   # N = 192 / 128 / g_s.7
         self.fwd = K.pack_conv(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, 16, it=self.it)
         # x6 forward (PixelShuffle store) and input gradient (PixelUnshuffle fill, the flipped weight)
         self.fwd6 = (K.pack_conv_x6(wr, self.R, self.Cin, 3, self.Cin * 9, 9, K.ORDER_DOWN, self.it)
@@ -152,7 +159,7 @@ class Subpel:
         # x6 at IT = 1 (g_s.7's 16 rho rows) is built for the bias epilogue only (ica_conv.hip pick_down_x6o)
         if self.fwd6 is not None and _x6_ok(kw) and (self.it != 1 or epi == K.EPI_BIAS):
             return K.conv_ex(x4, self.Cin, self.fwd6, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,
-                             alg_rows=4 * self.C, prec=K.PREC_X6, **kw)
+                             alg_rows=4 * self.C, prec=self.p6, **kw)
         return K.conv_ex(x4, self.Cin, self.fwd, self.bias, self.R, 3, 1, 0, epi, self.it, ps=True,
                          alg_rows=4 * self.C, **kw)
 
@@ -160,7 +167,7 @@ class Subpel:
         """g4: gradient of the shuffled output [N, C/4, 2H, 2W, 4] -> gradient of the input [N, Cin, H, W]."""
         if self.bwd6 is not None and _x6_ok(kw):
             return K.conv_ex(g4, self.R, self.bwd6, None, self.Cin, 3, 1, 0, K.EPI_BIAS, self.it_b,
-                             fill_mode=K.FILL_UNSHUFFLE, alg_rows=4 * self.C, prec=K.PREC_X6, **kw)
+                             fill_mode=K.FILL_UNSHUFFLE, alg_rows=4 * self.C, prec=self.p6, **kw)
         return K.conv_ex(g4, self.R, self.bwd, None, self.Cin, 3, 1, 0, K.EPI_BIAS, self.it_b,
                          fill_mode=K.FILL_UNSHUFFLE, alg_rows=4 * self.C, **kw)
 
@@ -172,7 +179,7 @@ def _gdn(sd, pre):
 class ChengAnalysis:
     """g_a = RBS(3,N) RB RBS RB RBS RB conv3x3 s2."""
 
-    def __init__(self, sd, prefix="g_a", tag="g_a", x6=False):
+    def __init__(self, sd, prefix="g_a", tag="g_a", x6=False, b1=False):
         self.tag = tag
         self.N = sd[_k(prefix, "6.weight")].shape[0]
         self.M = self.N
@@ -180,13 +187,13 @@ class ChengAnalysis:
         for i in range(6):
             pre = _k(prefix, str(i))
             if i % 2 == 0:
-                self.blocks.append(("rbs", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 2, x6=x6),
-                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6),
-                                    Conv3(sd[f"{pre}.skip.weight"], sd[f"{pre}.skip.bias"], 2, x6=x6),
+                self.blocks.append(("rbs", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 2, x6=x6, b1=b1),
+                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6, b1=b1),
+                                    Conv3(sd[f"{pre}.skip.weight"], sd[f"{pre}.skip.bias"], 2, x6=x6, b1=b1),
                                     _gdn(sd, f"{pre}.gdn")))
             else:
-                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6),
-                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6)))
+                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6, b1=b1),
+                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6, b1=b1)))
         self.last = Conv3(sd[_k(prefix, "6.weight")], sd[_k(prefix, "6.bias")], 2)
         # x6: the image-side block's two input gradients (conv1 k3 s2 and skip k1 s2 into 3 channels) as one fused
         # Z-gather launch (ica_conv_up3k3_x6) instead of two 32-row fp32 conv_up tiles computing 3 rows each
@@ -257,7 +264,7 @@ class ChengAnalysis:
 class ChengSynthesis:
     """g_s = RB RBU RB RBU RB RBU RB subpel_conv3x3(N, 3, 2)."""
 
-    def __init__(self, sd, prefix="g_s", tag="g_s", x6=False):
+    def __init__(self, sd, prefix="g_s", tag="g_s", x6=False, b1=False):
         self.tag = tag
         self.N = sd[_k(prefix, "0.conv1.weight")].shape[0]
         self.M = self.N
@@ -265,15 +272,15 @@ class ChengSynthesis:
         for i in range(7):
             pre = _k(prefix, str(i))
             if i % 2 == 0:
-                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6),
-                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6)))
+                self.blocks.append(("rb", Conv3(sd[f"{pre}.conv1.weight"], sd[f"{pre}.conv1.bias"], 1, x6=x6, b1=b1),
+                                    Conv3(sd[f"{pre}.conv2.weight"], sd[f"{pre}.conv2.bias"], 1, x6=x6, b1=b1)))
             else:
                 self.blocks.append(("rbu", Subpel(sd[f"{pre}.subpel_conv.0.weight"], sd[f"{pre}.subpel_conv.0.bias"],
-                                                  x6=x6),
-                                    Conv3(sd[f"{pre}.conv.weight"], sd[f"{pre}.conv.bias"], 1, x6=x6),
-                                    Subpel(sd[f"{pre}.upsample.0.weight"], sd[f"{pre}.upsample.0.bias"], x6=x6),
+                                                  x6=x6, b1=b1),
+                                    Conv3(sd[f"{pre}.conv.weight"], sd[f"{pre}.conv.bias"], 1, x6=x6, b1=b1),
+                                    Subpel(sd[f"{pre}.upsample.0.weight"], sd[f"{pre}.upsample.0.bias"], x6=x6, b1=b1),
                                     _gdn(sd, f"{pre}.igdn")))
-        self.last = Subpel(sd[_k(prefix, "7.0.weight")], sd[_k(prefix, "7.0.bias")], x6=x6)
+        self.last = Subpel(sd[_k(prefix, "7.0.weight")], sd[_k(prefix, "7.0.bias")], x6=x6, b1=b1)
 
     def forward(self, y4, save=False, inputs=None):
         """inputs: as ChengAnalysis.forward."""
@@ -403,15 +410,16 @@ class ChengKernels:
     model = "cheng2020"
 
     def __init__(self, sd: dict, precision: str = "fp32"):
-        """precision 'x6': the k3 s1 layers of g_a / g_s (the bulk of the work) on fp32-accurate bf16x6 operands;
-        strided, masked-fill and unshuffled-fill launches keep fp32 operands."""
+        """precision 'x6': the k3 layers of g_a / g_s (the bulk of the work) on fp32-accurate bf16x6 operands
+        (Conv3 / Subpel / rgb6 above list which launches); 'bf16': the same launches with the k3 conv_downs on bf16
+        operands over fp32 activations (hip_ops.PREC_B1; the stride-2 input gradients stay x6); the rest fp32."""
         if sd["g_a.6.weight"].device.type != "cuda":
             raise RuntimeError("ChengKernels needs the state dict on the HIP device")
-        if precision not in ("fp32", "x6"):
-            raise NotImplementedError(f"cheng2020 operands: fp32 or x6, not {precision!r}")
-        x6 = precision == "x6"
-        self.ga = ChengAnalysis(sd, x6=x6)
-        self.gs = ChengSynthesis(sd, x6=x6)
+        if precision not in ("fp32", "x6", "bf16"):
+            raise NotImplementedError(f"cheng2020 operands: fp32, x6 or bf16, not {precision!r}")
+        x6, b1 = precision in ("x6", "bf16"), precision == "bf16"
+        self.ga = ChengAnalysis(sd, x6=x6, b1=b1)
+        self.gs = ChengSynthesis(sd, x6=x6, b1=b1)
         self.N = self.M = self.ga.N
         self.ha = ChengHA(sd)
         self.hs = ChengHS(sd)

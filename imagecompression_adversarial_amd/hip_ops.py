@@ -88,7 +88,7 @@ def last_launch():
 PREC_HOOK = {}
 
 
-_PREC_SUFFIX = {0: "fp32", 1: "bf16", 2: "x6"}   # PREC_FP32, PREC_BF16, PREC_X6
+_PREC_SUFFIX = {0: "fp32", 1: "bf16", 2: "x6", 3: "b1"}   # PREC_FP32, PREC_BF16, PREC_X6, PREC_B1
 
 
 def _prec_note(tag, prec):
@@ -185,6 +185,9 @@ def pack_conv_bf16(w: torch.Tensor, O: int, Cc: int, KS: int, so: int, sc: int, 
 
 
 PREC_FP32, PREC_BF16, PREC_X6 = 0, 1, 2
+# bf16 operands over fp32 activations: the k3 conv_downs (cheng2020 --precision bf16) on the hi plane of the x6 pack
+# (RNE bf16 of activations and weights, fp32 accumulate, fp32 tensors; GDN epilogue GEMMs on the x6 gamma' pack)
+PREC_B1 = 3
 
 
 def x6_it(O: int) -> int:
@@ -507,7 +510,7 @@ def conv_ex(x4, Cin, wp, bias, Cout, KS, S, kind=0, epi=EPI_BIAS, it=0, gdn: Pac
         if prec == PREC_BF16:
             gdn.bf16()
             gp = gdn.gpbT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpb
-        elif prec == PREC_X6:   # x6 epilogue GEMMs (k5 s2 and, since round 4, the k3 s1 conv_downs)
+        elif prec in (PREC_X6, PREC_B1):   # x6 epilogue GEMMs (k5 s2 and, since round 4, the k3 s1 conv_downs)
             gdn.x6()
             gp = gdn.gpxT if epi in (EPI_GDN_BWD, EPI_IGDN_BWD) else gdn.gpx
         else:   # fp32 epilogues (fp32 operands)

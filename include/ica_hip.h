@@ -242,7 +242,12 @@ typedef struct ica_conv_args {
              * 2: fp32-accurate bf16x6 operands (wp from ica_pack_conv_weight_x6, gp from ica_pack_gdn_x6, fp32
              * x / y / saved tensors; k5 s2, Cin >= 16: conv_down BIAS/GDN/IGDN_BWD, conv_up BIAS/IGDN/GDN_BWD, 128 output channels,
              * or 96-multiples with the bias epilogue; k3 s1 conv_down (kind 0, it 4 or 6): every epilogue and fill
-             * mode except a save_t output, gp from ica_pack_gdn_x6 as well) */
+             * mode except a save_t output, gp from ica_pack_gdn_x6 as well);
+             * 3: bf16 operands over fp32 tensors on the k3 conv_downs (kind 0, KS 3: stride 1 as for prec 2, stride
+             * 2 plain-fill bias / leaky-ReLU forwards; it 4 or 6): wp from ica_pack_conv_weight_x6, of which only
+             * the hi plane (RNE bf16 of the weight) is read; the activation is rounded to bf16 (RNE) as it is
+             * staged; fp32 accumulate; GDN epilogue GEMMs on the ica_pack_gdn_x6 pack (cheng2020 --precision bf16,
+             * attack_rd.py:712-715) */
   int layout; /* parity-split pixel order (k5 s2, plain fill, no ps; 0 = row-major everywhere): bit 0 = x, bit 1 = y and
                * every other output-layout tensor (save_x / save_s, in_x / in_s, save_t, res).  A parity-split
                * H x W plane (H, W even) stores the four (y & 1, x & 1) sub-planes of (H/2) x (W/2) pixels one after

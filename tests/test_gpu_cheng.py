@@ -61,11 +61,11 @@ def test_conv_modes_vs_torch(K, Cin, Cout, KS, S, H, W):
 
 
 @pytest.mark.parametrize("H,W,res", [(64, 96, True), (32, 48, False), (96, 160, True)])
-def test_stride2_conv_input_gradient_x6(K, H, W, res):
+@pytest.mark.parametrize("C", [192, 128])
+def test_stride2_conv_input_gradient_x6(K, C, H, W, res):
     """The x6 input gradient of the stride-2 conv3x3 (cheng2020 g_a.2 / g_a.4 conv1: conv_up_x6 with KS = 3, IT = 6, a
     64-channel LDS group, bias + residual epilogue) against float64 autograd, at the fp32 tolerance."""
     from imagecompression_adversarial_amd.engine_cheng import Conv3
-    C = 192
     w = rnd((C, C, 3, 3), 21) / (C * 9) ** 0.5
     b = rnd((C,), 22) * 0.1
     c = Conv3(w.to(DEV), b.to(DEV), 2, x6=True)
@@ -81,11 +81,11 @@ def test_stride2_conv_input_gradient_x6(K, H, W, res):
 
 
 @pytest.mark.parametrize("H,W", [(64, 96), (96, 160), (256, 384)])
-def test_stride2_skip_input_gradient_x6(K, H, W):
+@pytest.mark.parametrize("C", [192, 128])
+def test_stride2_skip_input_gradient_x6(K, C, H, W):
     """The x6 input gradient of the 1x1 stride-2 skip (cheng2020 g_a.2 / g_a.4 skip: conv_up_x6 at KS = 1, one tap in
     output class (0, 0), zeros elsewhere) against float64 autograd at the fp32 tolerance."""
     from imagecompression_adversarial_amd.engine_cheng import Conv3
-    C = 192
     w = rnd((C, C, 1, 1), 28) / C ** 0.5
     b = rnd((C,), 29) * 0.1
     c = Conv3(w.to(DEV), b.to(DEV), 2, x6=True)
@@ -99,12 +99,12 @@ def test_stride2_skip_input_gradient_x6(K, H, W):
 
 
 @pytest.mark.parametrize("H,W", [(64, 96), (66, 94), (256, 384), (30, 34)])
-def test_stride2_conv_forward_x6(K, H, W):
+@pytest.mark.parametrize("C", [192, 128])
+def test_stride2_conv_forward_x6(K, C, H, W):
     """The x6 forward of the stride-2 conv3x3 (cheng2020 g_a.2 / g_a.4 conv1: the X6O conv_down at S = 2, its 2.5x
     larger patch filled two quads per tap; 32- and 16-px-wide tiles, tiles cut by the image edge, odd input sides)
     with the bias and leaky-ReLU epilogues, against float64 at the fp32 tolerance."""
     from imagecompression_adversarial_amd.engine_cheng import Conv3
-    C = 192
     w = rnd((C, C, 3, 3), 25) / (C * 9) ** 0.5
     b = rnd((C,), 26) * 0.1
     c = Conv3(w.to(DEV), b.to(DEV), 2, x6=True)
