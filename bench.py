@@ -466,10 +466,11 @@ def main():
     from imagecompression_adversarial_amd import codec as models
     from imagecompression_adversarial_amd import hip_ops as K
     from imagecompression_adversarial_amd.attack import AttackLoop
-    # the timed steps run eager, so that every tagged launch is bracketed by its own HIP events (the roofline's
-    # per-launch time over the timed region); the product's graph replay of the network step (attack.py) is off
-    # here unless ICA_BENCH_GRAPH=1 (then per_kernel_ms / roofline come from eager launches only and are absent)
-    A.ATTACK_GRAPH = os.environ.get("ICA_BENCH_GRAPH", "0") == "1"
+    # the timed steps run the product path: the whole-batch network step replayed as a HIP graph (attack.py; also
+    # for the ROI attack), no timing hooks.  ICA_BENCH_GRAPH=0 times them eager (A/B).  Per-kernel times, the
+    # roofline and the launch table come from a profiling pass right after the timed region: the same number of
+    # eager steps with every tagged launch bracketed by HIP events.
+    A.ATTACK_GRAPH = A.ATTACK_GRAPH and os.environ.get("ICA_BENCH_GRAPH", "1") != "0"
     from imagecompression_adversarial_amd.engine import CodecKernels
     from imagecompression_adversarial_amd.engine_cheng import ChengKernels
 
@@ -497,11 +498,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    K.EVENT_HOOK = {}
-    K.PREC_HOOK = {}
-    K.FLOPS_HOOK = {}
-    K.LAUNCH_HOOK = {}
-    exp0 = loop.expensive_image_steps()
+    exp0, rep0 = loop.expensive_image_steps(), loop.graph_replays
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
@@ -510,10 +507,23 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    exp_steps = loop.expensive_image_steps() - exp0   # image-steps of the timed window that ran the network
+    graph_replays = loop.graph_replays - rep0
+    # profiling pass: as many eager steps, every tagged launch timed by HIP events on its stream
+    graph_ok, loop.graph_ok = loop.graph_ok, False
+    K.EVENT_HOOK = {}
+    K.PREC_HOOK = {}
+    K.FLOPS_HOOK = {}
+    K.LAUNCH_HOOK = {}
+    exp1 = loop.expensive_image_steps()
+    for j in range(args.steps):
+        loop.step(min(args.warmup + args.steps + j, 1000))
+    torch.cuda.synchronize()
+    loop.graph_ok = graph_ok
+    prof_exp = loop.expensive_image_steps() - exp1
     hook, K.EVENT_HOOK = K.EVENT_HOOK, None
     table = _launch_table(K.LAUNCH_HOOK, rank)
     K.LAUNCH_HOOK = None
-    exp_steps = loop.expensive_image_steps() - exp0   # image-steps of the timed window that ran the network
     ranks = _rank_stats(dist, dev, el, B * args.steps, world)
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -625,6 +635,12 @@ def main():
                          "launch_ms": round(dom_ms, 4), "flops_per_launch": dom_flops},
             "branch_census": {"expensive_image_steps": exp_steps, "image_steps": B * args.steps,
                               "expensive_frac": round(exp_steps / (B * args.steps), 4)},
+            "timing": {"timed_steps": ("network step replayed as a HIP graph (product default)" if graph_replays
+                                       else "eager"),
+                       "graph_replays": graph_replays,
+                       "per_kernel_source": f"profiling pass: {args.steps} eager steps right after the timed region, "
+                                            "every tagged launch bracketed by HIP events on its stream",
+                       "profiling_pass_expensive_image_steps": prof_exp},
             "distributed": ranks,
             "full_run": full,
             "mixed_branch_run": mixed,

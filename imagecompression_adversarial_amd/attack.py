@@ -193,9 +193,10 @@ class AttackLoop:
         # wall time spent blocked in those waits (bench.py --mixed reports them)
         self.sync_steps = 0
         self.sync_wait_s = 0.0
-        # the whole-batch network step as a HIP graph (L2 losses; the ms-ssim loss path, the ROI attack and subclasses
-        # with their own network step -- the defended attack's, which reads its variant choice on the host -- run eager)
-        self.graph_ok = (ATTACK_GRAPH and dev.type == "cuda" and att_metric == "L2" and target is None
+        # the whole-batch network step as a HIP graph (L2 losses, the ROI attack's included; the ms-ssim loss path and
+        # subclasses with their own network step -- the defended attack's, which reads its variant choice on the host
+        # -- run eager)
+        self.graph_ok = (ATTACK_GRAPH and dev.type == "cuda" and att_metric == "L2"
                          and type(self).network_grad is AttackLoop.network_grad)
         self._graph, self._graph_out = None, None
         self.graph_replays = 0
@@ -350,7 +351,10 @@ class AttackLoop:
              self.eps, x0, x1, y0, y1, wit, wib, stream())
         K.reduce_rows(self.part, B, 1.0, out=self.loss_i)
         E, idx = self._select()
-        gx4 = self.network_grad(idx, E) if E > 0 else None
+        if E == B and idx is None and self.graph_ok:
+            gx4 = self._network_graph()
+        else:
+            gx4 = self.network_grad(idx, E) if E > 0 else None
         bc2s, neg_step = self._adam_scalars(i)
         call("ica_roi_adam", ptr(self.noise), ptr(self.im_s), ptr(gx4), ptr(self.loss_i), ptr(self.m), ptr(self.v),
              ptr(self.im_in if record_im_in else None), B, H, W, self.eps, self.thr, bc2s, neg_step,
