@@ -319,5 +319,5 @@ def adv_train_step(P, batch_x, steps=300, noise_thr=1e-4, epsilon=16.0, lr_attac
     aux_opt.zero_grad()
     aux_loss.backward()
     aux_opt.step()
-    return ({k: v.detach() for k, v in Q.items()}, {k: float(v.detach()) for k, v in out.items()}, float(aux_loss),
+    return ({k: v.detach() for k, v in Q.items()}, {k: float(v.detach()) for k, v in out.items()}, float(aux_loss.detach()),
             batch_adv)
