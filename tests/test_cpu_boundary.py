@@ -248,3 +248,15 @@ def test_old_format_checkpoint_conversion(tmp_path, capsys):
     coder.load_model(args3, training=False)
     out = capsys.readouterr().out
     assert "Trained epoch 4" in out and "Trained step 120" in out and "Learning rate: 0.0001" in out
+
+
+def test_b1_precision_code_documented():
+    """prec = 3 (bf16 operands over fp32 activations on the k3 conv_downs, cheng2020 --precision bf16) is the
+    hip_ops constant the C ABI header documents for ica_conv_args.prec."""
+    import os
+    from imagecompression_adversarial_amd import hip_ops as K
+    assert (K.PREC_FP32, K.PREC_BF16, K.PREC_X6, K.PREC_B1) == (0, 1, 2, 3)
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "ica_hip.h")).read()
+    assert "3: bf16 operands over fp32 tensors on the k3 conv_downs" in hdr
+    from imagecompression_adversarial_amd.engine_cheng import _it, X6_IT
+    assert _it(128) in X6_IT and _it(192) in X6_IT   # N = 128 and 192 both get the x6 / one-plane packs

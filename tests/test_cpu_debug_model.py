@@ -47,3 +47,17 @@ def test_oracle_debug_attack_unclamped_random_start():
     assert torch.equal(r0.noise, r.noise)       # the start is U(-sqrt(noise), sqrt(noise)) from the global RNG
     assert float((x + r.noise.clamp(-16 / 255, 16 / 255)).max()) > 1.0   # nothing clamps the input
     assert float(r.im_in.max()) > 1.0
+
+
+def test_debug_model_trainer_accepted():
+    """RDTrainer takes the debug model since round 6 (train_debug.DebugTrainStep; reference train.py:249-366 fine-tunes
+    whatever coder.load_model builds): the flat gradient buffer covers every main parameter, the EB quantiles stay
+    with the aux optimiser."""
+    from imagecompression_adversarial_amd.anchors import model as am
+    from imagecompression_adversarial_amd.train_engine import RDTrainer
+    net = am.init_model("debug", 3, "mse", pretrained=False)
+    tr = RDTrainer(net, "mse", 0.0483)
+    named = dict(net.named_parameters())
+    assert set(tr.names) == {k for k in named if not k.endswith(".quantiles")}
+    assert tr.flat_grad.numel() == sum(named[k].numel() for k in tr.names)
+    assert "g_a.0.weight" in tr.names and "g_s.0.weight" in tr.names and "h_s.0.weight" in tr.names
